@@ -1,0 +1,40 @@
+# Build of the MI355X-native RS coding path (gfx950 only).
+#   make            -> nexoedge_amd/lib/libnxec.so (+ C++ coding surface) and oracle/liboracle.so
+#   make ref        -> oracle/_ref (reference ISA-L base C, needs /root/reference; build container only)
+#   make golden     -> regenerate tests/golden/golden.json from oracle/_ref
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CXXSTD   := -std=c++17
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC $(CXXSTD) -Wall -Iinclude -Inexoedge_amd/csrc
+LIBDIR   := nexoedge_amd/lib
+CSRC     := nexoedge_amd/csrc
+OBJDIR   := build/obj
+
+LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip \
+            $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc
+LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
+HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(wildcard $(CSRC)/coding/*.hh)
+
+all: $(LIBDIR)/libnxec.so oracle/liboracle.so
+
+$(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libnxec.so: $(LIB_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(LIB_OBJS) -o $@
+
+oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_oracle.h
+	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c -o $@ -lpthread
+
+ref:
+	bash oracle/build_ref.sh
+
+golden: ref
+	oracle/_ref/gen_golden > tests/golden/golden.json
+
+clean:
+	rm -rf build $(LIBDIR)/libnxec.so oracle/liboracle.so
+
+.PHONY: all ref golden clean

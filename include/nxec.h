@@ -1,0 +1,201 @@
+/*
+ * nxec.h -- C ABI of the MI355X-native Reed-Solomon coding path for Nexoedge.
+ *
+ * The reference calls its GF(2^8) arithmetic through five ISA-L entry points
+ * (ISA-L 2.22 include/erasure_code.h:74,98,870,905,931), consumed by
+ * /root/reference/src/common/coding/rs.cc:26,27,89,104,106,196,219,229,230,290,316
+ * and coding_util.hh:20,21,27,28.  Section 1 below replaces those one-for-one
+ * (same argument meaning, same layouts); section 2 is the drop-in for
+ * ec_encode_data, executed on the GPU; sections 3-4 add the batched
+ * device-resident stripe API the proxy ChunkManager / agent use through
+ * RSCode (nexoedge_amd/csrc/coding/).  No torch types, no C++ types.
+ *
+ * Status codes: 0 ok, <0 error (nxec_last_error() says why).  There is no
+ * CPU fallback: every compute entry point runs a gfx950 HIP kernel, and
+ * fails with NXEC_ERR_NODEV when no device is usable.
+ *
+ * Thread safety: all entry points are re-entrant.  A context may be shared by
+ * threads (the reference shares one RSCode across proxy/agent workers,
+ * chunk_manager.cc:1779-1801); its host-staging slots are internally locked.
+ */
+#ifndef NXEC_H
+#define NXEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NXEC_OK 0
+#define NXEC_ERR_SINGULAR (-1) /* matrix not invertible (gf_invert_matrix's -1) */
+#define NXEC_ERR_INVALID (-2)  /* bad argument */
+#define NXEC_ERR_HIP (-3)      /* HIP runtime failure */
+#define NXEC_ERR_NOMEM (-4)
+#define NXEC_ERR_NODEV (-5)    /* no gfx950 device / HIP unavailable */
+
+#define NXEC_MAX_N 128 /* CODING_MAX_N, coding.hh:13 */
+#define NXEC_MAX_K 127
+
+/* last error message of the calling thread ("" if none) */
+const char *nxec_last_error(void);
+/* library version string */
+const char *nxec_version(void);
+
+/* ---------------------------------------------------------------------------
+ * 1. Host GF(2^8) math (poly 0x11d) -- replaces the ISA-L calls in rs.cc.
+ * ------------------------------------------------------------------------- */
+/* ISA-L gf_mul (erasure_code.h:905); used at rs.cc:219,316 */
+unsigned char nxec_gf_mul(unsigned char a, unsigned char b);
+/* ISA-L gf_inv; gf_inv(0) == 0 */
+unsigned char nxec_gf_inv(unsigned char a);
+/* ISA-L gf_gen_rs_matrix (erasure_code.h:870); rs.cc:26.  a: m x k row-major */
+void nxec_gf_gen_rs_matrix(unsigned char *a, int m, int k);
+/* ISA-L gf_invert_matrix (erasure_code.h:931); rs.cc:196,290.  Like ISA-L it
+ * clobbers `in`.  Returns 0, or -1 if singular. */
+int nxec_gf_invert_matrix(unsigned char *in, unsigned char *out, const int n);
+/* ISA-L ec_init_tables (erasure_code.h:74); rs.cc:27,104,229, coding_util.hh:20,27.
+ * gftbls: 32 bytes per coefficient, rows x k, ISA-L layout
+ * ([0..15] = c*x, [16..31] = c*(x<<4)); byte [1] of each is the coefficient. */
+void nxec_ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbls);
+
+/* ---------------------------------------------------------------------------
+ * 2. Drop-in synchronous host-buffer encode -- replaces ISA-L ec_encode_data
+ *    (erasure_code.h:98) at rs.cc:89,106,230 and coding_util.hh:21,28.
+ *    coding[r][i] = XOR_j c(r,j) * data[j][i], c from gftbls (byte [1]).
+ *    Runs on the calling thread's current device (a per-device default
+ *    context), staging through pinned memory.  The void form aborts with a
+ *    message on failure (the ISA-L signature has no error channel and silent
+ *    corruption is not an option); the _status form returns the error.
+ * ------------------------------------------------------------------------- */
+void nxec_ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
+                         unsigned char **coding);
+int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gftbls,
+                               const unsigned char *const *data, unsigned char *const *coding);
+/* same, taking the rows x k coefficient matrix directly (no 32-B tables) */
+int nxec_encode_host(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                     unsigned char *const *coding);
+
+/* nxec_encode_host plus fused pass-through: for j < k with copy_idx[j] >= 0,
+ * data[j] is also delivered to copy_out[copy_idx[j]] by the same GPU pass
+ * (the unit rows of a full-output decode, rs.cc:228-230).  rows may be 0. */
+int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                        unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out);
+
+/* ---------------------------------------------------------------------------
+ * 3. Contexts and batched device-resident stripe ops.
+ *    Layout: stripe s, chunk c starts at base + s*stripe_stride + c*chunk_stride.
+ *    `stream` is a hipStream_t (NULL = the context's stream).  Launches are
+ *    asynchronous on that stream; buffers must stay valid until it drains.
+ * ------------------------------------------------------------------------- */
+typedef struct nxec_ctx nxec_ctx_t;
+
+int nxec_ctx_create(int device, nxec_ctx_t **out);
+void nxec_ctx_destroy(nxec_ctx_t *ctx);
+void *nxec_ctx_stream(nxec_ctx_t *ctx);
+
+/* The one primitive behind encode, recover, repair, agent partial encode and
+ * CAR finalize: for every stripe s and byte i < len,
+ *   dst(s, dst_idx[r])[i] = XOR_{j<k} coeffs[r*k + j] (x) src(s, src_idx[j])[i],  r < rows.
+ * src_idx / dst_idx: chunk indices (NULL = 0..k-1 / 0..rows-1).
+ * copy_idx (optional, NULL = none): for j < k with copy_idx[j] >= 0 the raw
+ * source chunk is also written to dst chunk copy_idx[j] (fused survivor copy
+ * of a full-output decode, rs.cc:175-181 semantics).
+ * rows, k in 1..NXEC_MAX_K; len >= 0; nstripes >= 0. */
+int nxec_stripes_mul(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
+                     const int32_t *src_idx, int64_t src_chunk_stride, int64_t src_stripe_stride,
+                     unsigned char *d_dst, const int32_t *dst_idx, int64_t dst_chunk_stride,
+                     int64_t dst_stripe_stride, const int32_t *copy_idx, int64_t len, int64_t nstripes,
+                     void *stream);
+
+/* Gather form for non-contiguous chunks: d_src_ptrs is a DEVICE array of
+ * nstripes*k device pointers ([s][j]), d_dst_ptrs of nstripes*rows. */
+int nxec_stripes_mul_ptrs(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs,
+                          const unsigned char *const *d_src_ptrs, unsigned char *const *d_dst_ptrs, int64_t len,
+                          int64_t nstripes, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * 4. RSCode-level batched ops over the [stripe][n][len] layout
+ *    (RS with nexoedge's (n, k): n total chunks, k data chunks).
+ * ------------------------------------------------------------------------- */
+/* RSCode::encode (rs.cc:57-92) for a batch: chunks k..n-1 of every stripe are
+ * computed from chunks 0..k-1. */
+int nxec_rs_encode_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_stripes, int64_t chunk_stride,
+                           int64_t stripe_stride, int64_t len, int64_t nstripes, void *stream);
+
+/* Recover-only decode / repair in place: rebuilds the `nfailed` chunks listed
+ * in `failed` (ascending) from the first k alive chunks, exactly the plan of
+ * RSCode::preDecode(isRepair=true) (rs.cc:238-322).  Erased slots are only
+ * written, never read. */
+int nxec_rs_recover_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                            unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride, int64_t len,
+                            int64_t nstripes, void *stream);
+
+/* Full-output decode with RSCode::decode semantics (rs.cc:111-236, non-repair):
+ * inputs = the first k alive chunks of d_stripes (ascending ids; `failed`
+ * lists the erased ids), output = all k data chunks into d_out
+ * ([s][j] at d_out + s*out_stripe_stride + j*out_chunk_stride).  Survivor data
+ * chunks are copied from registers in the same pass (bit-identical to the
+ * reference's unit rows of the inverse). */
+int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                           const unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride,
+                           unsigned char *d_out, int64_t out_chunk_stride, int64_t out_stripe_stride, int64_t len,
+                           int64_t nstripes, void *stream);
+
+/* Host-resident batch encode (the proxy write path): h_data [s][k][len] in,
+ * h_parity [s][n-k][len] out, both host memory (pinned/registered memory is
+ * DMA'd directly; pageable memory is staged).  Double-buffered H2D -> kernel
+ * -> D2H over `batch_stripes` stripes per step.  Synchronous. */
+int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data,
+                              unsigned char *h_parity, int64_t len, int64_t nstripes, int64_t batch_stripes);
+
+/* Host planning of RSCode::preDecode (rs.cc:238-322): input_ids gets every
+ * alive id ascending (n - nfailed of them, *ninputs), *min_inputs = k; with
+ * is_repair the nfailed x k repair matrix goes to repair_matrix.  Returns 0,
+ * NXEC_ERR_INVALID (too many failures) or NXEC_ERR_SINGULAR. */
+int nxec_rs_plan(int n, int k, const int32_t *failed, int nfailed, int is_repair, int32_t *input_ids,
+                 int *ninputs, int *min_inputs, unsigned char *repair_matrix);
+/* Decode matrix rows (rs.cc:141-225): given the k ascending input ids, the
+ * coefficient rows (ntargets x k) that rebuild each target id. */
+int nxec_rs_decode_matrix(int n, int k, const int32_t *input_ids, const int32_t *targets, int ntargets,
+                          unsigned char *out);
+
+/* ---------------------------------------------------------------------------
+ * 5. Device plumbing (memory, streams, events) so hosts without a GPU
+ *    framework can drive section 3.  Thin wrappers over the HIP runtime.
+ * ------------------------------------------------------------------------- */
+int nxec_device_count(int *count);
+int nxec_set_device(int device);
+int nxec_device_info(int device, char *name, int name_len, int *num_cus, int64_t *total_mem);
+int nxec_dev_malloc(void **p, size_t bytes);
+int nxec_dev_free(void *p);
+int nxec_host_malloc_pinned(void **p, size_t bytes);
+int nxec_host_free_pinned(void *p);
+int nxec_host_register(void *p, size_t bytes);
+int nxec_host_unregister(void *p);
+int nxec_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes, void *stream);
+int nxec_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes, void *stream);
+int nxec_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes, void *stream);
+int nxec_memset(void *d_dst, int value, size_t bytes, void *stream);
+int nxec_stream_create(void **stream);
+int nxec_stream_destroy(void *stream);
+int nxec_stream_sync(void *stream);
+int nxec_device_sync(void);
+int nxec_event_create(void **event);
+int nxec_event_destroy(void *event);
+int nxec_event_record(void *event, void *stream);
+int nxec_event_elapsed_ms(void *start, void *stop, float *ms);
+/* deterministic device fill: the splitmix64 byte stream (word i = mix(seed + (i+1)*0x9E3779B97F4A7C15), LE) */
+int nxec_fill_random(void *d_dst, size_t bytes, uint64_t seed, void *stream);
+/* order-sensitive 64-bit digest of a device buffer: sum_i word_i * (2i+1) (mod 2^64), tail bytes zero-padded */
+int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream);
+
+/* Describe the launch nxec_stripes_mul would use (kernel variant, LDS
+ * replication, block/grid) -- for benchmarks and logs. */
+int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NXEC_H */

@@ -1,0 +1,107 @@
+"""ctypes loader for libnxec.so (the C ABI in include/nxec.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) into
+``nexoedge_amd/lib/libnxec.so``.  Importing this module fails loudly when it
+is missing: there is no Python or CPU fallback for the coding kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnxec.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libnxec.so not found at {LIB_PATH}; build it with `make` (or __graft_entry__.build()). "
+        "nexoedge_amd has no CPU fallback."
+    )
+
+lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+
+u8p = C.POINTER(C.c_ubyte)
+i32p = C.POINTER(C.c_int32)
+vp = C.c_void_p
+i64 = C.c_int64
+
+_PROTOS = {
+    "nxec_last_error": (C.c_char_p, []),
+    "nxec_version": (C.c_char_p, []),
+    "nxec_gf_mul": (C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
+    "nxec_gf_inv": (C.c_ubyte, [C.c_ubyte]),
+    "nxec_gf_gen_rs_matrix": (None, [vp, C.c_int, C.c_int]),
+    "nxec_gf_invert_matrix": (C.c_int, [vp, vp, C.c_int]),
+    "nxec_ec_init_tables": (None, [C.c_int, C.c_int, vp, vp]),
+    "nxec_ec_encode_data": (None, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
+    "nxec_ec_encode_data_status": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
+    "nxec_encode_host": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
+    "nxec_encode_host_ex": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
+    "nxec_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+    "nxec_ctx_destroy": (None, [vp]),
+    "nxec_ctx_stream": (vp, [vp]),
+    "nxec_stripes_mul": (
+        C.c_int,
+        [vp, C.c_int, C.c_int, vp, vp, vp, i64, i64, vp, vp, i64, i64, vp, i64, i64, vp],
+    ),
+    "nxec_stripes_mul_ptrs": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, vp, i64, i64, vp]),
+    "nxec_rs_encode_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, i64, vp]),
+    "nxec_rs_recover_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, i64, vp]),
+    "nxec_rs_decode_stripes": (
+        C.c_int,
+        [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, i64, vp],
+    ),
+    "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
+    "nxec_rs_plan": (C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
+    "nxec_rs_decode_matrix": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp]),
+    "nxec_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "nxec_set_device": (C.c_int, [C.c_int]),
+    "nxec_device_info": (C.c_int, [C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(i64)]),
+    "nxec_dev_malloc": (C.c_int, [C.POINTER(vp), C.c_size_t]),
+    "nxec_dev_free": (C.c_int, [vp]),
+    "nxec_host_malloc_pinned": (C.c_int, [C.POINTER(vp), C.c_size_t]),
+    "nxec_host_free_pinned": (C.c_int, [vp]),
+    "nxec_host_register": (C.c_int, [vp, C.c_size_t]),
+    "nxec_host_unregister": (C.c_int, [vp]),
+    "nxec_memcpy_h2d": (C.c_int, [vp, vp, C.c_size_t, vp]),
+    "nxec_memcpy_d2h": (C.c_int, [vp, vp, C.c_size_t, vp]),
+    "nxec_memcpy_d2d": (C.c_int, [vp, vp, C.c_size_t, vp]),
+    "nxec_memset": (C.c_int, [vp, C.c_int, C.c_size_t, vp]),
+    "nxec_stream_create": (C.c_int, [C.POINTER(vp)]),
+    "nxec_stream_destroy": (C.c_int, [vp]),
+    "nxec_stream_sync": (C.c_int, [vp]),
+    "nxec_device_sync": (C.c_int, []),
+    "nxec_event_create": (C.c_int, [C.POINTER(vp)]),
+    "nxec_event_destroy": (C.c_int, [vp]),
+    "nxec_event_record": (C.c_int, [vp, vp]),
+    "nxec_event_elapsed_ms": (C.c_int, [vp, vp, C.POINTER(C.c_float)]),
+    "nxec_fill_random": (C.c_int, [vp, C.c_size_t, C.c_uint64, vp]),
+    "nxec_checksum": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), vp]),
+    "nxec_describe_launch": (C.c_int, [vp, C.c_int, C.c_int, i64, i64, C.c_char_p, C.c_int]),
+}
+
+for _name, (_res, _args) in _PROTOS.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = tuple(_PROTOS)
+
+NXEC_OK = 0
+NXEC_ERR_SINGULAR = -1
+NXEC_ERR_INVALID = -2
+NXEC_ERR_HIP = -3
+NXEC_ERR_NOMEM = -4
+NXEC_ERR_NODEV = -5
+
+
+class NxecError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        msg = lib.nxec_last_error().decode(errors="replace")
+        super().__init__(f"{what} failed ({code}): {msg}")
+        self.code = code
+
+
+def check(rc: int, what: str) -> None:
+    if rc != NXEC_OK:
+        raise NxecError(rc, what)

@@ -1,0 +1,202 @@
+// RSCode on MI355X.  Behaviour follows /root/reference/src/common/coding/rs.cc
+// (line numbers cited per method); arithmetic runs in libnxec's gfx950
+// kernels (nxec_encode_host / nxec_encode_host_ex), host code only plans.
+#include "rs.hh"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+// rs.cc:11-30
+RSCode::RSCode(CodingOptions options) {
+  const coding_param_t n = options.getN(), k = options.getK();
+  if (n <= 0 || k <= 0 || n < k) throw std::invalid_argument("RS codes only support n>=k, n > 0, and k > 0");
+  _options = options;
+  _name = "RS";
+  nxec_gf_gen_rs_matrix(_encodeMatrix, n, k);  // rs.cc:26
+}
+
+num_t RSCode::getNumDataChunks() { return _options.getK(); }
+num_t RSCode::getNumCodeChunks() { return _options.getN() - _options.getK(); }
+num_t RSCode::getNumChunks() { return _options.getN(); }
+num_t RSCode::getNumChunksPerNode() { return 1; }
+length_t RSCode::getCodingStateSize() { return 0; }
+
+// rs.cc:52-55: ceil(dataSize / k)
+length_t RSCode::getChunkSize(length_t dataSize) {
+  const coding_param_t k = _options.getK();
+  return (dataSize + k - 1) / k;
+}
+
+// rs.cc:57-92: n chunks (32-B aligned), data chunks copied from `data`
+// (caller zero-pads to k*chunkSize), parity computed on the GPU.
+bool RSCode::encode(data_t *data, length_t dataSize, std::vector<Chunk> &stripe, data_t ** /*codingState*/) {
+  const int k = _options.getK(), n = _options.getN();
+  const length_t cs = getChunkSize(dataSize);
+  stripe.clear();
+  stripe.resize(n);
+  std::vector<const unsigned char *> datap(k);
+  std::vector<unsigned char *> codep(n - k > 0 ? n - k : 1);
+  for (int i = 0; i < n; i++) {
+    stripe.at(i).setChunkId(i);
+    if (!stripe.at(i).allocateData(static_cast<int>(cs), /* aligned */ true)) {
+      std::fprintf(stderr, "RSCode: failed to allocate chunk %d of %u bytes\n", i, cs);
+      stripe.clear();
+      return false;
+    }
+    if (i < k) {
+      std::memcpy(stripe.at(i).data, data + static_cast<size_t>(i) * cs, cs);
+      datap[i] = stripe.at(i).data;
+    } else {
+      codep[i - k] = stripe.at(i).data;
+    }
+  }
+  if (n == k || cs == 0) return true;
+  const int rc = nxec_encode_host(static_cast<int>(cs), k, n - k, _encodeMatrix + k * k, datap.data(), codep.data());
+  if (rc != NXEC_OK) {
+    std::fprintf(stderr, "RSCode::encode: %s\n", nxec_last_error());
+    stripe.clear();
+    return false;
+  }
+  return true;
+}
+
+// rs.cc:94-109: one partial -> copy; G partials -> XOR (all-ones 1 x G row)
+bool RSCode::carRepairFinalize(unsigned char *inputp[], num_t numInputChunks, length_t chunkSize,
+                               unsigned char *decodep[]) {
+  if (numInputChunks == 1) {
+    std::memcpy(decodep[0], inputp[0], chunkSize);
+    return true;
+  }
+  std::vector<unsigned char> ones(numInputChunks, 1);
+  return nxec_encode_host(static_cast<int>(chunkSize), static_cast<int>(numInputChunks), 1, ones.data(), inputp,
+                          decodep) == NXEC_OK;
+}
+
+// rs.cc:111-236
+bool RSCode::decode(std::vector<Chunk> &inputChunks, data_t **decodedData, length_t &decodedSize,
+                    DecodingPlan & /*plan*/, data_t * /*codingState*/, bool isRepair,
+                    std::vector<chunk_id_t> repairTargets) {
+  const int k = _options.getK(), n = _options.getN();
+  const num_t numInputs = static_cast<num_t>(inputChunks.size());
+  const length_t cs = inputChunks.empty() ? 0 : static_cast<length_t>(inputChunks.at(0).size);
+  const bool targetsGiven = !repairTargets.empty();
+
+  if (numInputs < static_cast<num_t>(k) && (!isRepair || !_options.repairUsingCAR())) {  // rs.cc:134-137
+    std::fprintf(stderr, "RSCode: insufficient input chunks (%u < %d)\n", numInputs, k);
+    return false;
+  }
+  // inputs are matched to ids positionally and must be ascending (rs.cc:142-158)
+  std::vector<int32_t> ids;
+  for (int i = 0, idx = 0; i < n; i++) {
+    if (idx < static_cast<int>(numInputs) && inputChunks.at(idx).chunkId == i) {
+      ids.push_back(i);
+      idx++;
+    } else if (isRepair && !targetsGiven) {
+      repairTargets.push_back(static_cast<chunk_id_t>(i));
+    }
+  }
+  const num_t numDecoded = isRepair ? static_cast<num_t>(repairTargets.size()) : static_cast<num_t>(k);
+
+  data_t *out = *decodedData;
+  if (out == nullptr) {  // rs.cc:164-173
+    out = static_cast<data_t *>(std::malloc(static_cast<size_t>(numDecoded) * cs + 1));
+    if (!out) return false;
+  }
+  std::vector<unsigned char *> decodep(numDecoded > 0 ? numDecoded : 1);
+  for (num_t i = 0; i < numDecoded; i++) decodep[i] = out + static_cast<size_t>(i) * cs;
+  decodedSize = numDecoded * cs;
+  std::vector<unsigned char *> inputp(numInputs > 0 ? numInputs : 1);
+  for (num_t i = 0; i < numInputs; i++) inputp[i] = inputChunks.at(i).data;
+
+  auto fail = [&]() {
+    if (*decodedData != out) std::free(out);
+    return false;
+  };
+
+  if (isRepair && numDecoded == 1 && _options.repairUsingCAR()) {  // rs.cc:184-192
+    if (!carRepairFinalize(inputp.data(), numInputs, cs, decodep.data())) return fail();
+    *decodedData = out;
+    return true;
+  }
+  if (ids.size() < static_cast<size_t>(k)) return fail();
+  if (cs == 0) {
+    *decodedData = out;
+    return true;
+  }
+
+  if (isRepair) {  // rs.cc:204-225: inverse rows for data targets, enc_row x inverse for parity targets
+    std::vector<int32_t> tg(repairTargets.begin(), repairTargets.end());
+    std::vector<unsigned char> m(static_cast<size_t>(tg.size()) * k + 1);
+    if (nxec_rs_decode_matrix(n, k, ids.data(), tg.data(), static_cast<int>(tg.size()), m.data()) != NXEC_OK)
+      return fail();
+    if (nxec_encode_host(static_cast<int>(cs), k, static_cast<int>(tg.size()), m.data(), inputp.data(),
+                         decodep.data()) != NXEC_OK)
+      return fail();
+  } else {
+    // all k data chunks (rs.cc:228-230 with the k x k inverse): rows of the
+    // inverse for erased data ids, and the unit rows of surviving data ids
+    // realised as copies fused into the same GPU pass.
+    std::vector<int32_t> tg, copy(k, -1);
+    std::vector<bool> present(k, false);
+    for (int j = 0; j < k; j++)
+      if (ids[j] < k) {
+        present[ids[j]] = true;
+        copy[j] = ids[j];
+      }
+    for (int d = 0; d < k; d++)
+      if (!present[d]) tg.push_back(d);
+    std::vector<unsigned char> m(static_cast<size_t>(tg.size()) * k + 1);
+    if (!tg.empty() && nxec_rs_decode_matrix(n, k, ids.data(), tg.data(), static_cast<int>(tg.size()), m.data()))
+      return fail();
+    std::vector<unsigned char *> tp(tg.size() + 1);
+    for (size_t t = 0; t < tg.size(); t++) tp[t] = decodep[tg[t]];
+    if (nxec_encode_host_ex(static_cast<int>(cs), k, static_cast<int>(tg.size()), m.data(), inputp.data(), tp.data(),
+                            copy.data(), decodep.data()) != NXEC_OK)
+      return fail();
+  }
+  *decodedData = out;
+  return true;
+}
+
+// rs.cc:238-322
+bool RSCode::preDecode(const std::vector<chunk_id_t> &failed, DecodingPlan &plan, data_t * /*codingState*/,
+                       bool isRepair) {
+  const int k = _options.getK(), n = _options.getN();
+  const int nf = static_cast<int>(failed.size());
+  if (nf > n - k) return false;  // rs.cc:244-247
+  plan.release();
+  std::vector<int32_t> f(failed.begin(), failed.end()), inputs(n);
+  std::vector<unsigned char> rm(static_cast<size_t>(nf > 0 ? nf : 1) * k);
+  int ni = 0, mi = 0;
+  if (nxec_rs_plan(n, k, f.data(), nf, isRepair ? 1 : 0, inputs.data(), &ni, &mi, rm.data()) != NXEC_OK) {
+    plan.release();
+    return false;
+  }
+  for (int i = 0; i < ni; i++) plan.addInputChunkId(static_cast<chunk_id_t>(inputs[i]));
+  plan.setMinNumInputChunks(static_cast<num_t>(mi));
+  if (isRepair) {
+    if (!plan.allocateRepairMatrix(static_cast<length_t>(nf) * k)) {
+      plan.release();
+      return false;
+    }
+    if (nf > 0) std::memcpy(plan.getRepairMatrix(), rm.data(), static_cast<size_t>(nf) * k);
+  }
+  return true;
+}
+
+bool RSCode::encodeStripes(nxec_ctx_t *ctx, unsigned char *dStripes, int64_t chunkStride, int64_t stripeStride,
+                           int64_t chunkSize, int64_t numStripes, void *stream) {
+  return nxec_rs_encode_stripes(ctx, _options.getN(), _options.getK(), dStripes, chunkStride, stripeStride, chunkSize,
+                                numStripes, stream) == NXEC_OK;
+}
+
+bool RSCode::recoverStripes(nxec_ctx_t *ctx, const std::vector<chunk_id_t> &failed, unsigned char *dStripes,
+                            int64_t chunkStride, int64_t stripeStride, int64_t chunkSize, int64_t numStripes,
+                            void *stream) {
+  std::vector<int32_t> f(failed.begin(), failed.end());
+  return nxec_rs_recover_stripes(ctx, _options.getN(), _options.getK(), f.data(), static_cast<int>(f.size()),
+                                 dStripes, chunkStride, stripeStride, chunkSize, numStripes, stream) == NXEC_OK;
+}

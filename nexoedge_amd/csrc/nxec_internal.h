@@ -1,0 +1,63 @@
+// Internal declarations shared by the host runtime and the HIP kernels of libnxec.
+#ifndef NXEC_INTERNAL_H
+#define NXEC_INTERNAL_H
+
+#include <cstdint>
+#include <vector>
+
+#include "nxec.h"
+
+namespace nxec {
+
+// Sets the calling thread's last-error message and returns `code`.
+int set_error(int code, const char *fmt, ...);
+bool valid_nk(int n, int k);
+int repair_rows(int n, int k, const std::vector<uint8_t> &enc, const int32_t *input_ids, const int32_t *targets,
+                int ntargets, uint8_t *out);
+
+constexpr int kMaxRowsPerPass = 4;  // one packed 32-bit LDS entry holds 4 row products
+
+// Kernel arguments of one GF(2^8) stripe-multiply pass (<= 4 output rows).
+// Chunk (s, c) of the source lives at src + s*src_stripe_stride + c*src_chunk_stride
+// (strided mode) or at src_ptrs[s*k + j] (gather mode, src_ptrs != nullptr).
+struct MulArgs {
+  const uint8_t *src;
+  uint8_t *dst;
+  const uint8_t *const *src_ptrs;
+  uint8_t *const *dst_ptrs;
+  int64_t src_chunk_stride, src_stripe_stride;
+  int64_t dst_chunk_stride, dst_stripe_stride;
+  int64_t len;         // bytes per chunk
+  int64_t vec_count;   // 16-byte vectors per chunk handled by the vector kernel
+  int64_t byte_begin;  // first byte handled by the byte kernel
+  int64_t nstripes;
+  int32_t k, rows;
+  int32_t any_copy;                 // copy_idx has entries >= 0
+  int32_t dst_ptr_row0;             // gather mode: first row of this pass inside dst_ptrs[s*rows_total + r]
+  int32_t dst_ptr_rows;             // gather mode: rows_total
+  int16_t src_idx[NXEC_MAX_K + 1];
+  int16_t dst_idx[kMaxRowsPerPass];
+  int16_t copy_idx[NXEC_MAX_K + 1];  // -1 = none
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // row-major rows x k
+};
+
+struct LaunchInfo {
+  const char *variant;
+  int lds_copies;   // R: table replication factor
+  int block;        // threads per workgroup
+  int grid;         // workgroups
+  int lds_bytes;
+};
+
+// Chooses and describes the vector-kernel launch for (k, len, nstripes).
+LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool gather);
+// Enqueues one pass (vector kernel + byte kernel for tails / misaligned data).
+int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
+// Raises the dynamic-LDS limit of every kernel instantiation (once per device).
+int prepare_kernels();
+int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream);
+int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
+
+}  // namespace nxec
+
+#endif

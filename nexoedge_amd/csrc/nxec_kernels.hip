@@ -1,0 +1,373 @@
+// gfx950 (CDNA4) kernels of the Nexoedge RS coding path.
+//
+// One primitive: dst_r[i] = XOR_j c(r,j) (x) src_j[i] over GF(2^8)/0x11d, for
+// r < rows <= 4 and every byte i of every stripe in a batch.  This is the work
+// of ISA-L's ec_encode_data (ec_base.c:302-317; SIMD gf_4vect_dot_prod_*.asm)
+// as called by rs.cc:89 (encode), rs.cc:230 (decode/repair), rs.cc:106 (CAR
+// XOR) and coding_util.hh:21,28 (agent partial encode) -- re-designed for
+// MI355X rather than translated:
+//
+//  * Table lookup in LDS.  For every source j the workgroup builds a
+//    256-entry table whose 32-bit entry x packs the products c(r,j)*x of all
+//    (<= 4) output rows.  One ds_read_b32 per source byte yields every row's
+//    product at once, so each data byte is read from HBM once and looked up
+//    once, whatever the number of rows (the reference's SIMD kernel and the
+//    "one wavefront per row" alternative both re-touch the data per row).
+//  * Bank-conflict-free-ish replication.  Random data bytes make LDS bank
+//    conflicts data dependent; table copy c = lane % R sits in the bank bits
+//    (address = ((j*256 + x)*R + c)*4), so with R = 16 a half-wave's 32 lanes
+//    collide at most pairwise (4 LDS cycles per wave lookup instead of ~8 at
+//    R = 1).  R = 16 for k <= 10 (k*16 KiB of LDS), R = 8 for k <= 20.
+//  * HBM side: each lane owns one 16-byte column vector of the stripe; a wave
+//    issues k global_load_dwordx4 (1 KiB contiguous per source, all k in
+//    flight) and `rows` global_store_dwordx4 after an in-register 4x4 byte
+//    transpose (v_perm_b32) of the packed accumulators.
+//  * Persistent grid (one or two 1024-thread workgroups per CU) walks the
+//    flattened (stripe, column-tile) space, so the tables are built once per
+//    workgroup, not per tile.
+//  * No MFMA: this is byte-wise lookup/XOR work bounded by HBM bandwidth.
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
+
+#include "nxec_internal.h"
+
+namespace nxec {
+
+namespace {
+
+constexpr int kBlock = 1024;       // threads per workgroup (16 waves)
+constexpr int kMaxTemplK = 20;     // k with a fully unrolled kernel; larger k use the dynamic kernel
+constexpr int kLdsBytes = 160 * 1024;
+
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p ^= (b & 1u) ? a : 0u;
+    a = (a << 1) ^ ((a & 0x80u) ? 0x11du : 0u);
+    b >>= 1;
+  }
+  return p;
+}
+
+// entry x of source j: byte r = c(r, j) * x
+template <int R>
+__device__ __forceinline__ void build_tables(const MulArgs &a, int k, uint32_t *tab) {
+  for (int i = threadIdx.x; i < k * 256; i += blockDim.x) {
+    const int j = i >> 8;
+    const uint32_t x = static_cast<uint32_t>(i & 255);
+    uint32_t e = 0;
+    for (int r = 0; r < a.rows; r++) e |= gf_mul_dev(a.coef[r * a.k + j], x) << (8 * r);
+#pragma unroll
+    for (int c = 0; c < R; c++) tab[i * R + c] = e;
+  }
+}
+
+// Chunk addresses of stripe s.  GATHER is a template parameter so the
+// per-source address math stays branch-free (uniform, SGPR-resident).
+template <bool GATHER>
+__device__ __forceinline__ uint8_t *dst_row(const MulArgs &a, uint32_t s, int r) {
+  if (GATHER) return a.dst_ptrs[static_cast<size_t>(s) * a.dst_ptr_rows + a.dst_ptr_row0 + r];
+  return a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + a.dst_idx[r] * a.dst_chunk_stride;
+}
+
+template <bool GATHER>
+__device__ __forceinline__ const uint8_t *src_chunk(const MulArgs &a, uint32_t s, int j) {
+  if (GATHER) return a.src_ptrs[static_cast<size_t>(s) * a.k + j];
+  return a.src + static_cast<int64_t>(s) * a.src_stripe_stride + a.src_idx[j] * a.src_chunk_stride;
+}
+
+// acc[p] holds the 4 row products of column byte p (p = 4q + b); write row r's
+// 16 bytes = byte r of acc[0..15].  8 v_perm_b32 per 4 columns.
+template <bool GATHER>
+__device__ __forceinline__ void store_rows(const MulArgs &a, uint32_t s, uint32_t v, const uint32_t acc[16]) {
+  uint32_t o[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
+    const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);
+    const uint32_t hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
+    const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+    const uint32_t hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+    o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+    o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+    o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+    o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+  }
+#pragma unroll
+  for (int r = 0; r < kMaxRowsPerPass; r++) {
+    if (r < a.rows) reinterpret_cast<uint4 *>(dst_row<GATHER>(a, s, r))[v] = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
+  }
+}
+
+template <int R>
+__device__ __forceinline__ void lookup16(const char *tb, const uint4 d, uint32_t acc[16]) {
+  const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t x = (w[q] >> (8 * b)) & 0xffu;
+      acc[4 * q + b] ^= *reinterpret_cast<const uint32_t *>(tb + x * (4 * R));
+    }
+  }
+}
+
+// Fully unrolled vector kernel: all K source loads of a column vector in flight.
+template <int K, int R, bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
+  extern __shared__ uint32_t tab[];
+  build_tables<R>(a, K, tab);
+  __syncthreads();
+  const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
+  const uint32_t tps = (nvec + kBlock - 1) / kBlock;
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  const char *tlane = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tps;
+    const uint32_t v = (t - s * tps) * kBlock + threadIdx.x;
+    if (v >= nvec) continue;
+    uint4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) d[j] = reinterpret_cast<const uint4 *>(src_chunk<GATHER>(a, s, j))[v];
+    uint32_t acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) lookup16<R>(tlane + j * 1024 * R, d[j], acc);
+    store_rows<GATHER>(a, s, v, acc);
+    if (!GATHER && a.any_copy) {
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        const int c = a.copy_idx[j];
+        if (c >= 0)
+          reinterpret_cast<uint4 *>(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride)[v] =
+              d[j];
+      }
+    }
+  }
+}
+
+// Runtime-k vector kernel (k > kMaxTemplK), R = 1 tables, sources in groups of 4.
+template <bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_mul_vec_dyn(const MulArgs a) {
+  extern __shared__ uint32_t tab[];
+  const int k = a.k;
+  build_tables<1>(a, k, tab);
+  __syncthreads();
+  const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
+  const uint32_t tps = (nvec + kBlock - 1) / kBlock;
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  const char *tl = reinterpret_cast<const char *>(tab);
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t s = t / tps;
+    const uint32_t v = (t - s * tps) * kBlock + threadIdx.x;
+    if (v >= nvec) continue;
+    uint32_t acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0;
+    for (int j0 = 0; j0 < k; j0 += 4) {
+      uint4 d[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++)
+        if (j0 + jj < k) d[jj] = reinterpret_cast<const uint4 *>(src_chunk<GATHER>(a, s, j0 + jj))[v];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        if (j0 + jj < k) {
+          lookup16<1>(tl + (j0 + jj) * 1024, d[jj], acc);
+          const int c = a.copy_idx[j0 + jj];
+          if (!GATHER && a.any_copy && c >= 0)
+            reinterpret_cast<uint4 *>(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride)[v] =
+                d[jj];
+        }
+      }
+    }
+    store_rows<GATHER>(a, s, v, acc);
+  }
+}
+
+// Byte-granular kernel: chunk tails past vec_count*16 and misaligned layouts.
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_mul_bytes(const MulArgs a) {
+  extern __shared__ uint32_t tab[];
+  const int k = a.k;
+  build_tables<1>(a, k, tab);
+  __syncthreads();
+  const int64_t span = a.len - a.byte_begin;
+  const int64_t total = span * a.nstripes;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t s = static_cast<uint32_t>(i / span);
+    const int64_t pos = a.byte_begin + (i - static_cast<int64_t>(s) * span);
+    uint32_t acc = 0;
+    for (int j = 0; j < k; j++) {
+      const uint8_t x = src_chunk<GATHER>(a, s, j)[pos];
+      acc ^= tab[j * 256 + x];
+      const int c = a.copy_idx[j];
+      if (!GATHER && a.any_copy && c >= 0) a.dst[static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride + pos] = x;
+    }
+    for (int r = 0; r < a.rows; r++) dst_row<GATHER>(a, s, r)[pos] = static_cast<uint8_t>(acc >> (8 * r));
+  }
+}
+
+__global__ void k_fill(uint8_t *p, int64_t bytes, uint64_t seed) {
+  const int64_t words = (bytes + 7) / 8;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < words;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    uint64_t z = seed + static_cast<uint64_t>(i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    if (aligned && (i + 1) * 8 <= bytes) {
+      reinterpret_cast<uint64_t *>(p)[i] = z;
+    } else {
+      for (int b = 0; b < 8 && i * 8 + b < bytes; b++) p[i * 8 + b] = static_cast<uint8_t>(z >> (8 * b));
+    }
+  }
+}
+
+__global__ void k_checksum(const uint8_t *p, int64_t bytes, unsigned long long *out) {
+  const int64_t words = (bytes + 7) / 8;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
+  uint64_t acc = 0;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < words;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    uint64_t w = 0;
+    if (aligned && (i + 1) * 8 <= bytes) {
+      w = reinterpret_cast<const uint64_t *>(p)[i];
+    } else {
+      for (int b = 0; b < 8 && i * 8 + b < bytes; b++) w |= static_cast<uint64_t>(p[i * 8 + b]) << (8 * b);
+    }
+    acc += w * static_cast<uint64_t>(2 * i + 1);
+  }
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, static_cast<unsigned long long>(acc));
+}
+
+using KernelFn = void (*)(MulArgs);
+
+template <int R, bool G, int... Ks>
+constexpr std::array<KernelFn, sizeof...(Ks)> vec_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_mul_vec<Ks + 1, R, G>...}};
+}
+
+// strided form: every (k, R) for tuning; gather form: the default R only
+const auto kVecR16 = vec_table<16, false>(std::make_integer_sequence<int, 10>{});        // k = 1..10
+const auto kVecR8 = vec_table<8, false>(std::make_integer_sequence<int, kMaxTemplK>{});  // k = 1..20
+const auto kVecR1 = vec_table<1, false>(std::make_integer_sequence<int, kMaxTemplK>{});  // k = 1..20
+const auto kVecG16 = vec_table<16, true>(std::make_integer_sequence<int, 10>{});         // k = 1..10
+const auto kVecG8 = vec_table<8, true>(std::make_integer_sequence<int, kMaxTemplK>{});   // k = 1..20
+
+int hip_fail(hipError_t e, const char *what) {
+  return set_error(NXEC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+// LDS replication policy (NXEC_LDS_R=1|8|16 overrides, for tuning only).
+int choose_r(int k) {
+  const char *env = std::getenv("NXEC_LDS_R");
+  int want = env ? std::atoi(env) : 0;
+  if (k > kMaxTemplK) return 1;
+  if (want == 1) return 1;
+  if (want == 8) return 8;
+  if (want == 16 && k <= 10) return 16;
+  return k <= 10 ? 16 : 8;
+}
+
+KernelFn vec_kernel(int k, int r, bool gather) {
+  if (k > kMaxTemplK) return gather ? &k_mul_vec_dyn<true> : &k_mul_vec_dyn<false>;
+  if (gather) return k <= 10 ? kVecG16[k - 1] : kVecG8[k - 1];
+  if (r == 16) return kVecR16[k - 1];
+  if (r == 8) return kVecR8[k - 1];
+  return kVecR1[k - 1];
+}
+
+// gather kernels always use the default replication
+int gather_r(int k) { return k > kMaxTemplK ? 1 : (k <= 10 ? 16 : 8); }
+
+}  // namespace
+
+LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool gather) {
+  LaunchInfo li{};
+  li.lds_copies = gather ? gather_r(k) : choose_r(k);
+  li.block = kBlock;
+  li.lds_bytes = k * 1024 * li.lds_copies;
+  int per_cu = kLdsBytes / (li.lds_bytes > 0 ? li.lds_bytes : 1);
+  if (per_cu > 2) per_cu = 2;  // 2 x 16 waves = the CU's 32-wave limit
+  if (per_cu < 1) per_cu = 1;
+  const int64_t tps = (vec_count + kBlock - 1) / kBlock;
+  int64_t ntiles = tps * nstripes;
+  int64_t grid = static_cast<int64_t>(num_cus) * per_cu;
+  if (grid > ntiles) grid = ntiles;
+  li.grid = static_cast<int>(grid);
+  li.variant = k > kMaxTemplK ? "vec_dyn" : "vec_unrolled";
+  return li;
+}
+
+int prepare_kernels() {
+  auto raise = [](KernelFn fn, int lds) -> hipError_t {
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  };
+  for (int k = 1; k <= kMaxTemplK; k++) {
+    for (int r : {1, 8, 16}) {
+      if (r == 16 && k > 10) continue;
+      hipError_t e = raise(vec_kernel(k, r, false), k * 1024 * r);
+      if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec)");
+    }
+    hipError_t e = raise(vec_kernel(k, gather_r(k), true), k * 1024 * gather_r(k));
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec gather)");
+  }
+  for (KernelFn fn : {&k_mul_vec_dyn<false>, &k_mul_vec_dyn<true>, &k_mul_bytes<false>, &k_mul_bytes<true>}) {
+    hipError_t e = raise(fn, NXEC_MAX_K * 1024);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(dyn/bytes)");
+  }
+  return NXEC_OK;
+}
+
+int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (a.nstripes <= 0 || a.len <= 0) return NXEC_OK;
+  if (vec_ok && a.vec_count > 0) {
+    const int64_t tps = (a.vec_count + kBlock - 1) / kBlock;
+    if (tps * a.nstripes >= (int64_t(1) << 32) || a.vec_count >= (int64_t(1) << 32))
+      return set_error(NXEC_ERR_INVALID, "batch too large for one launch (split nstripes)");
+    const bool gather = a.src_ptrs != nullptr;
+    LaunchInfo li = plan_launch(a.k, a.vec_count, a.nstripes, num_cus, gather);
+    KernelFn fn = vec_kernel(a.k, li.lds_copies, gather);
+    hipLaunchKernelGGL(fn, dim3(li.grid), dim3(li.block), li.lds_bytes, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "launch k_mul_vec");
+  }
+  if (a.byte_begin < a.len) {
+    const int64_t total = (a.len - a.byte_begin) * a.nstripes;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > static_cast<int64_t>(num_cus) * 8) blocks = static_cast<int64_t>(num_cus) * 8;
+    KernelFn fn = a.src_ptrs ? &k_mul_bytes<true> : &k_mul_bytes<false>;
+    hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(blocks)), dim3(256), a.k * 1024, st, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "launch k_mul_bytes");
+  }
+  return NXEC_OK;
+}
+
+int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream) {
+  if (bytes == 0) return NXEC_OK;
+  hipLaunchKernelGGL(k_fill, dim3(2048), dim3(256), 0, static_cast<hipStream_t>(stream), static_cast<uint8_t *>(d),
+                     static_cast<int64_t>(bytes), seed);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_fill");
+}
+
+int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream) {
+  hipLaunchKernelGGL(k_checksum, dim3(1024), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t *>(d), static_cast<int64_t>(bytes),
+                     reinterpret_cast<unsigned long long *>(d_out));
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_checksum");
+}
+
+}  // namespace nxec

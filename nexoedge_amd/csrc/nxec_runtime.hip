@@ -1,0 +1,650 @@
+// Host runtime of libnxec: contexts, argument validation, the RS batch entry
+// points and the drop-in host-buffer encode.  Compute always goes to the
+// gfx950 kernels in nxec_kernels.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "nxec.h"
+#include "nxec_internal.h"
+
+namespace nxec {
+
+namespace {
+thread_local std::string g_last_error;
+
+// A host-staging slot: pinned + device buffers and a stream, used by the
+// synchronous host-buffer entry points.  Slots are pooled per context so
+// concurrent callers (proxy workers, agent threads) do not serialize.
+struct Slot {
+  hipStream_t stream = nullptr;
+  uint8_t *h = nullptr;
+  uint8_t *d = nullptr;
+  size_t cap = 0;
+};
+}  // namespace
+
+int set_error(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+static int hip_err(hipError_t e, const char *what) {
+  return set_error(e == hipErrorNoDevice || e == hipErrorInvalidDevice ? NXEC_ERR_NODEV : NXEC_ERR_HIP, "%s: %s", what,
+                   hipGetErrorString(e));
+}
+
+#define NXEC_HIP(call)                           \
+  do {                                           \
+    hipError_t e_ = (call);                      \
+    if (e_ != hipSuccess) return hip_err(e_, #call); \
+  } while (0)
+
+}  // namespace nxec
+
+using namespace nxec;
+
+struct nxec_ctx {
+  int device = 0;
+  int num_cus = 0;
+  hipStream_t stream = nullptr;
+  std::mutex slot_mu;
+  std::vector<Slot *> free_slots;
+  std::vector<Slot *> all_slots;
+};
+
+namespace {
+
+std::mutex g_prep_mu;
+std::vector<bool> g_prepared;
+
+int ensure_device(int device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return set_error(NXEC_ERR_NODEV, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= count) return set_error(NXEC_ERR_NODEV, "device %d out of range (%d devices)", device, count);
+  NXEC_HIP(hipSetDevice(device));
+  std::lock_guard<std::mutex> lk(g_prep_mu);
+  if (g_prepared.size() < static_cast<size_t>(count)) g_prepared.resize(count, false);
+  if (!g_prepared[device]) {
+    hipDeviceProp_t prop;
+    NXEC_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return set_error(NXEC_ERR_NODEV, "device %d is %s; libnxec is built for gfx950 only", device, prop.gcnArchName);
+    int rc = prepare_kernels();
+    if (rc) return rc;
+    g_prepared[device] = true;
+  }
+  return NXEC_OK;
+}
+
+bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
+  Slot *s = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ctx->slot_mu);
+    if (!ctx->free_slots.empty()) {
+      s = ctx->free_slots.back();
+      ctx->free_slots.pop_back();
+    }
+  }
+  if (!s) {
+    s = new Slot();
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete s;
+      return hip_err(e, "hipStreamCreate(slot)");
+    }
+    std::lock_guard<std::mutex> lk(ctx->slot_mu);
+    ctx->all_slots.push_back(s);
+  }
+  if (s->cap < bytes) {
+    if (s->h) (void)hipHostFree(s->h);
+    if (s->d) (void)hipFree(s->d);
+    s->h = nullptr;
+    s->d = nullptr;
+    s->cap = 0;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s->h), bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&s->d), bytes);
+    if (e != hipSuccess) {
+      std::lock_guard<std::mutex> lk(ctx->slot_mu);
+      ctx->free_slots.push_back(s);
+      return hip_err(e, "staging allocation");
+    }
+    s->cap = bytes;
+  }
+  *out = s;
+  return NXEC_OK;
+}
+
+void release_slot(nxec_ctx_t *ctx, Slot *s) {
+  std::lock_guard<std::mutex> lk(ctx->slot_mu);
+  ctx->free_slots.push_back(s);
+}
+
+std::mutex g_default_mu;
+std::vector<nxec_ctx_t *> g_default_ctx;
+
+int default_ctx(nxec_ctx_t **out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  if (g_default_ctx.size() <= static_cast<size_t>(dev)) g_default_ctx.resize(dev + 1, nullptr);
+  if (!g_default_ctx[dev]) {
+    int rc = nxec_ctx_create(dev, &g_default_ctx[dev]);
+    if (rc) return rc;
+  }
+  *out = g_default_ctx[dev];
+  return NXEC_OK;
+}
+
+hipStream_t pick_stream(nxec_ctx_t *ctx, void *stream) {
+  return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// Shared implementation of the strided and gather forms.
+int stripes_mul_impl(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
+                     const unsigned char *const *d_src_ptrs, const int32_t *src_idx, int64_t src_cs, int64_t src_ss,
+                     unsigned char *d_dst, unsigned char *const *d_dst_ptrs, const int32_t *dst_idx, int64_t dst_cs,
+                     int64_t dst_ss, const int32_t *copy_idx, int64_t len, int64_t nstripes, void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  const bool gather = d_src_ptrs != nullptr;
+  bool any_copy = false;
+  if (copy_idx)
+    for (int j = 0; j < k; j++) any_copy |= copy_idx[j] >= 0;
+  if (k < 1 || k > NXEC_MAX_K || rows < 0 || rows > NXEC_MAX_K || (rows == 0 && !any_copy))
+    return set_error(NXEC_ERR_INVALID, "rows=%d k=%d out of range", rows, k);
+  if (len < 0 || nstripes < 0) return set_error(NXEC_ERR_INVALID, "negative len or nstripes");
+  if (rows > 0 && !coeffs) return set_error(NXEC_ERR_INVALID, "null coefficient matrix");
+  if (len == 0 || nstripes == 0) return NXEC_OK;
+  if (gather) {
+    if (!d_dst_ptrs) return set_error(NXEC_ERR_INVALID, "gather form needs both pointer tables");
+  } else if (!d_src || (!d_dst && (rows > 0 || any_copy))) {
+    return set_error(NXEC_ERR_INVALID, "null stripe buffer");
+  }
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+
+  MulArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.src = d_src;
+  a.dst = d_dst;
+  a.src_ptrs = d_src_ptrs;
+  a.dst_ptrs = d_dst_ptrs;
+  a.src_chunk_stride = src_cs;
+  a.src_stripe_stride = src_ss;
+  a.dst_chunk_stride = dst_cs;
+  a.dst_stripe_stride = dst_ss;
+  a.len = len;
+  a.nstripes = nstripes;
+  a.k = k;
+  a.dst_ptr_rows = rows;
+  for (int j = 0; j < k; j++) {
+    const int32_t si = src_idx ? src_idx[j] : j;
+    if (si < 0 || si > 32767) return set_error(NXEC_ERR_INVALID, "src_idx[%d]=%d out of range", j, si);
+    a.src_idx[j] = static_cast<int16_t>(si);
+    const int32_t ci = copy_idx ? copy_idx[j] : -1;
+    if (ci > 32767) return set_error(NXEC_ERR_INVALID, "copy_idx[%d]=%d out of range", j, ci);
+    a.copy_idx[j] = static_cast<int16_t>(ci < 0 ? -1 : ci);
+  }
+  if (gather && any_copy) return set_error(NXEC_ERR_INVALID, "copy_idx is only supported in the strided form");
+
+  bool vec_ok = true;
+  if (!gather) {
+    vec_ok = aligned16(d_src) && aligned16(d_dst) && (src_cs % 16 == 0) && (src_ss % 16 == 0) &&
+             (dst_cs % 16 == 0) && (dst_ss % 16 == 0);
+  }
+  // gather form: the kernels assume 16-byte aligned chunk pointers
+  const int64_t vec_count = vec_ok ? len / 16 : 0;
+  a.vec_count = vec_count;
+  a.byte_begin = vec_count * 16;
+
+  // split nstripes so one launch's tile count fits 32 bits
+  const int64_t tps = std::max<int64_t>(1, (vec_count + 1023) / 1024);
+  const int64_t max_stripes = std::max<int64_t>(1, ((int64_t(1) << 31) / tps));
+
+  const int passes = rows == 0 ? 1 : (rows + kMaxRowsPerPass - 1) / kMaxRowsPerPass;
+  for (int p = 0; p < passes; p++) {
+    const int r0 = p * kMaxRowsPerPass;
+    const int pr = std::min(kMaxRowsPerPass, rows - r0);
+    a.rows = std::max(pr, 0);
+    a.any_copy = (p == 0 && any_copy) ? 1 : 0;
+    a.dst_ptr_row0 = r0;
+    for (int r = 0; r < kMaxRowsPerPass; r++) {
+      const int rr = r0 + r;
+      int32_t di = 0;
+      if (r < pr) {
+        di = dst_idx ? dst_idx[rr] : rr;
+        if (di < 0 || di > 32767) return set_error(NXEC_ERR_INVALID, "dst_idx[%d]=%d out of range", rr, di);
+      }
+      a.dst_idx[r] = static_cast<int16_t>(di);
+      for (int j = 0; j < k; j++) a.coef[r * k + j] = r < pr ? coeffs[static_cast<size_t>(rr) * k + j] : 0;
+    }
+    for (int64_t s0 = 0; s0 < nstripes; s0 += max_stripes) {
+      MulArgs b = a;
+      b.nstripes = std::min(max_stripes, nstripes - s0);
+      if (gather) {
+        b.src_ptrs = d_src_ptrs + s0 * k;
+        b.dst_ptrs = d_dst_ptrs + s0 * rows;
+      } else {
+        b.src = d_src + s0 * src_ss;
+        b.dst = d_dst ? d_dst + s0 * dst_ss : nullptr;
+      }
+      rc = launch_mul(b, vec_ok, ctx->num_cus, st);
+      if (rc) return rc;
+    }
+  }
+  return NXEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *nxec_last_error(void) { return g_last_error.c_str(); }
+const char *nxec_version(void) { return "nxec 0.1.0 gfx950"; }
+
+int nxec_ctx_create(int device, nxec_ctx_t **out) {
+  if (!out) return set_error(NXEC_ERR_INVALID, "null out pointer");
+  *out = nullptr;
+  int rc = ensure_device(device);
+  if (rc) return rc;
+  std::unique_ptr<nxec_ctx_t> ctx(new nxec_ctx_t());
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  NXEC_HIP(hipGetDeviceProperties(&prop, device));
+  ctx->num_cus = prop.multiProcessorCount;
+  NXEC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  *out = ctx.release();
+  return NXEC_OK;
+}
+
+void nxec_ctx_destroy(nxec_ctx_t *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+  }
+  for (Slot *s : ctx->all_slots) {
+    if (s->stream) {
+      (void)hipStreamSynchronize(s->stream);
+      (void)hipStreamDestroy(s->stream);
+    }
+    if (s->h) (void)hipHostFree(s->h);
+    if (s->d) (void)hipFree(s->d);
+    delete s;
+  }
+  delete ctx;
+}
+
+void *nxec_ctx_stream(nxec_ctx_t *ctx) { return ctx ? static_cast<void *>(ctx->stream) : nullptr; }
+
+int nxec_stripes_mul(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
+                     const int32_t *src_idx, int64_t src_chunk_stride, int64_t src_stripe_stride,
+                     unsigned char *d_dst, const int32_t *dst_idx, int64_t dst_chunk_stride,
+                     int64_t dst_stripe_stride, const int32_t *copy_idx, int64_t len, int64_t nstripes,
+                     void *stream) {
+  return stripes_mul_impl(ctx, rows, k, coeffs, d_src, nullptr, src_idx, src_chunk_stride, src_stripe_stride, d_dst,
+                          nullptr, dst_idx, dst_chunk_stride, dst_stripe_stride, copy_idx, len, nstripes, stream);
+}
+
+int nxec_stripes_mul_ptrs(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs,
+                          const unsigned char *const *d_src_ptrs, unsigned char *const *d_dst_ptrs, int64_t len,
+                          int64_t nstripes, void *stream) {
+  if (!d_src_ptrs) return set_error(NXEC_ERR_INVALID, "null source pointer table");
+  if (rows < 1) return set_error(NXEC_ERR_INVALID, "rows must be >= 1");
+  return stripes_mul_impl(ctx, rows, k, coeffs, nullptr, d_src_ptrs, nullptr, 0, 0, nullptr, d_dst_ptrs, nullptr, 0,
+                          0, nullptr, len, nstripes, stream);
+}
+
+int nxec_rs_encode_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_stripes, int64_t chunk_stride,
+                           int64_t stripe_stride, int64_t len, int64_t nstripes, void *stream) {
+  if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
+  if (n == k) return NXEC_OK;
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);  // rs.cc:26
+  std::vector<int32_t> dst(n - k);
+  for (int i = k; i < n; i++) dst[i - k] = i;
+  return nxec_stripes_mul(ctx, n - k, k, enc.data() + static_cast<size_t>(k) * k, d_stripes, nullptr, chunk_stride,
+                          stripe_stride, d_stripes, dst.data(), chunk_stride, stripe_stride, nullptr, len, nstripes,
+                          stream);
+}
+
+int nxec_rs_recover_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                            unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride, int64_t len,
+                            int64_t nstripes, void *stream) {
+  if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
+  if (nfailed == 0) return NXEC_OK;
+  std::vector<int32_t> inputs(n);
+  std::vector<uint8_t> rm(static_cast<size_t>(std::max(nfailed, 1)) * k);
+  int ni = 0, mi = 0;
+  int rc = nxec_rs_plan(n, k, failed, nfailed, 1, inputs.data(), &ni, &mi, rm.data());  // rs.cc:238-322
+  if (rc) return rc;
+  return nxec_stripes_mul(ctx, nfailed, k, rm.data(), d_stripes, inputs.data(), chunk_stride, stripe_stride,
+                          d_stripes, failed, chunk_stride, stripe_stride, nullptr, len, nstripes, stream);
+}
+
+int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                           const unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride,
+                           unsigned char *d_out, int64_t out_chunk_stride, int64_t out_stripe_stride, int64_t len,
+                           int64_t nstripes, void *stream) {
+  if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
+  std::vector<int32_t> inputs(n);
+  int ni = 0, mi = 0;
+  int rc = nxec_rs_plan(n, k, failed, nfailed, 0, inputs.data(), &ni, &mi, nullptr);  // rs.cc:252-265
+  if (rc) return rc;
+  // erased data chunks get inverse rows (rs.cc:196,228-230); surviving data
+  // chunks are unit rows of the inverse, i.e. copies of their input.
+  std::vector<int32_t> targets, copy(k, -1);
+  for (int i = 0; i < nfailed; i++)
+    if (failed[i] < k) targets.push_back(failed[i]);
+  for (int j = 0; j < k; j++)
+    if (inputs[j] < k) copy[j] = inputs[j];
+  std::vector<uint8_t> m(std::max<size_t>(1, targets.size() * k));
+  if (!targets.empty()) {
+    rc = nxec_rs_decode_matrix(n, k, inputs.data(), targets.data(), static_cast<int>(targets.size()), m.data());
+    if (rc) return rc;
+  }
+  return stripes_mul_impl(ctx, static_cast<int>(targets.size()), k, m.data(), d_stripes, nullptr, inputs.data(),
+                          chunk_stride, stripe_stride, d_out, nullptr, targets.data(), out_chunk_stride,
+                          out_stripe_stride, copy.data(), len, nstripes, stream);
+}
+
+int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,
+                              int64_t len, int64_t nstripes, int64_t batch_stripes) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  if (!valid_nk(n, k) || len < 0 || nstripes < 0) return set_error(NXEC_ERR_INVALID, "invalid arguments");
+  if (n == k || len == 0 || nstripes == 0) return NXEC_OK;
+  if (!h_data || !h_parity) return set_error(NXEC_ERR_INVALID, "null host buffer");
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  const int p = n - k;
+  if (batch_stripes <= 0) batch_stripes = std::max<int64_t>(1, (int64_t(256) << 20) / (len * n));
+  batch_stripes = std::min(batch_stripes, nstripes);
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);
+  constexpr int kSlots = 3;
+  const size_t dbytes = static_cast<size_t>(batch_stripes) * k * len, pbytes = static_cast<size_t>(batch_stripes) * p * len;
+  uint8_t *dbuf[kSlots] = {}, *pbuf[kSlots] = {};
+  hipStream_t streams[kSlots] = {};
+  auto cleanup = [&]() {
+    for (int i = 0; i < kSlots; i++) {
+      if (streams[i]) {
+        (void)hipStreamSynchronize(streams[i]);
+        (void)hipStreamDestroy(streams[i]);
+      }
+      if (dbuf[i]) (void)hipFree(dbuf[i]);
+      if (pbuf[i]) (void)hipFree(pbuf[i]);
+    }
+  };
+  for (int i = 0; i < kSlots; i++) {
+    hipError_t e = hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&dbuf[i]), dbytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&pbuf[i]), pbytes);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_err(e, "encode_host_batch setup");
+    }
+  }
+  int64_t b = 0;
+  for (int64_t s0 = 0; s0 < nstripes; s0 += batch_stripes, b++) {
+    const int slot = static_cast<int>(b % kSlots);
+    const int64_t ns = std::min(batch_stripes, nstripes - s0);
+    hipStream_t st = streams[slot];
+    hipError_t e = hipMemcpyAsync(dbuf[slot], h_data + s0 * k * len, static_cast<size_t>(ns) * k * len,
+                                  hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_err(e, "H2D");
+    }
+    rc = nxec_stripes_mul(ctx, p, k, enc.data() + static_cast<size_t>(k) * k, dbuf[slot], nullptr, len, k * len,
+                          pbuf[slot], nullptr, len, p * len, nullptr, len, ns, st);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+    e = hipMemcpyAsync(h_parity + s0 * p * len, pbuf[slot], static_cast<size_t>(ns) * p * len, hipMemcpyDeviceToHost,
+                       st);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_err(e, "D2H");
+    }
+  }
+  for (int i = 0; i < kSlots; i++) {
+    hipError_t e = hipStreamSynchronize(streams[i]);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_err(e, "encode_host_batch sync");
+    }
+  }
+  cleanup();
+  return NXEC_OK;
+}
+
+int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                        unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out) {
+  int ncopy = 0;
+  if (copy_idx)
+    for (int j = 0; j < k; j++) ncopy = std::max(ncopy, copy_idx[j] + 1);
+  if (len < 0 || k < 1 || k > NXEC_MAX_K || rows < 0 || (rows == 0 && ncopy == 0) || !data ||
+      (rows > 0 && (!coeffs || !coding)) || (ncopy > 0 && !copy_out))
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_host: invalid arguments");
+  if (len == 0) return NXEC_OK;
+  nxec_ctx_t *ctx = nullptr;
+  int rc = default_ctx(&ctx);
+  if (rc) return rc;
+  const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;  // keep chunks 16-B aligned in staging
+  const int nchunks = k + rows + ncopy;
+  Slot *slot = nullptr;
+  rc = acquire_slot(ctx, static_cast<size_t>(stride) * nchunks, &slot);
+  if (rc) return rc;
+  for (int j = 0; j < k; j++) std::memcpy(slot->h + j * stride, data[j], static_cast<size_t>(len));
+  hipError_t e = hipMemcpyAsync(slot->d, slot->h, static_cast<size_t>(stride) * k, hipMemcpyHostToDevice, slot->stream);
+  if (e != hipSuccess) {
+    release_slot(ctx, slot);
+    return hip_err(e, "H2D");
+  }
+  // staging layout: [k inputs][rows outputs][ncopy pass-through outputs]
+  std::vector<int32_t> dst(std::max(rows, 1)), cpy(k, -1);
+  for (int r = 0; r < rows; r++) dst[r] = k + r;
+  for (int j = 0; j < k; j++)
+    if (copy_idx && copy_idx[j] >= 0) cpy[j] = k + rows + copy_idx[j];
+  rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d, nullptr, stride, 0, slot->d, dst.data(), stride, 0,
+                        ncopy ? cpy.data() : nullptr, len, 1, slot->stream);
+  if (rc == NXEC_OK) {
+    e = hipMemcpyAsync(slot->h + stride * k, slot->d + stride * k, static_cast<size_t>(stride) * (rows + ncopy),
+                       hipMemcpyDeviceToHost, slot->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(slot->stream);
+    if (e != hipSuccess) rc = hip_err(e, "D2H/sync");
+  }
+  if (rc == NXEC_OK) {
+    for (int r = 0; r < rows; r++) std::memcpy(coding[r], slot->h + (k + r) * stride, static_cast<size_t>(len));
+    for (int j = 0; j < k; j++)
+      if (copy_idx && copy_idx[j] >= 0)
+        std::memcpy(copy_out[copy_idx[j]], slot->h + (k + rows + copy_idx[j]) * stride, static_cast<size_t>(len));
+  }
+  release_slot(ctx, slot);
+  return rc;
+}
+
+int nxec_encode_host(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                     unsigned char *const *coding) {
+  if (rows < 1) return set_error(NXEC_ERR_INVALID, "nxec_encode_host: rows must be >= 1");
+  return nxec_encode_host_ex(len, k, rows, coeffs, data, coding, nullptr, nullptr);
+}
+
+int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gftbls, const unsigned char *const *data,
+                               unsigned char *const *coding) {
+  if (!gftbls || k < 1 || rows < 1) return set_error(NXEC_ERR_INVALID, "nxec_ec_encode_data: invalid arguments");
+  // byte [1] of each 32-byte ISA-L table is c*1 = c (gf_vect_mul_init, ec_base.c:169-274)
+  std::vector<uint8_t> coeffs(static_cast<size_t>(rows) * k);
+  for (size_t i = 0; i < coeffs.size(); i++) coeffs[i] = gftbls[32 * i + 1];
+  return nxec_encode_host(len, k, rows, coeffs.data(), data, coding);
+}
+
+void nxec_ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
+                         unsigned char **coding) {
+  int rc = nxec_ec_encode_data_status(len, k, rows, gftbls, data, coding);
+  if (rc != NXEC_OK) {
+    std::fprintf(stderr, "nxec_ec_encode_data failed (%d): %s\n", rc, nxec_last_error());
+    std::abort();
+  }
+}
+
+// ---- plumbing ----
+
+int nxec_device_count(int *count) {
+  if (!count) return set_error(NXEC_ERR_INVALID, "null pointer");
+  *count = 0;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_err(e, "hipGetDeviceCount");
+  }
+  return NXEC_OK;
+}
+
+int nxec_set_device(int device) { return ensure_device(device); }
+
+int nxec_device_info(int device, char *name, int name_len, int *num_cus, int64_t *total_mem) {
+  hipDeviceProp_t prop;
+  NXEC_HIP(hipGetDeviceProperties(&prop, device));
+  if (name && name_len > 0) std::snprintf(name, name_len, "%s", prop.gcnArchName);
+  if (num_cus) *num_cus = prop.multiProcessorCount;
+  if (total_mem) *total_mem = static_cast<int64_t>(prop.totalGlobalMem);
+  return NXEC_OK;
+}
+
+int nxec_dev_malloc(void **p, size_t bytes) {
+  if (!p) return set_error(NXEC_ERR_INVALID, "null pointer");
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) return set_error(NXEC_ERR_NOMEM, "hipMalloc(%zu): out of memory", bytes);
+  NXEC_HIP(e);
+  return NXEC_OK;
+}
+int nxec_dev_free(void *p) {
+  NXEC_HIP(hipFree(p));
+  return NXEC_OK;
+}
+int nxec_host_malloc_pinned(void **p, size_t bytes) {
+  if (!p) return set_error(NXEC_ERR_INVALID, "null pointer");
+  NXEC_HIP(hipHostMalloc(p, bytes, hipHostMallocDefault));
+  return NXEC_OK;
+}
+int nxec_host_free_pinned(void *p) {
+  NXEC_HIP(hipHostFree(p));
+  return NXEC_OK;
+}
+int nxec_host_register(void *p, size_t bytes) {
+  NXEC_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return NXEC_OK;
+}
+int nxec_host_unregister(void *p) {
+  NXEC_HIP(hipHostUnregister(p));
+  return NXEC_OK;
+}
+int nxec_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes, void *stream) {
+  NXEC_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes, void *stream) {
+  NXEC_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes, void *stream) {
+  NXEC_HIP(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_memset(void *d_dst, int value, size_t bytes, void *stream) {
+  NXEC_HIP(hipMemsetAsync(d_dst, value, bytes, static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_stream_create(void **stream) {
+  if (!stream) return set_error(NXEC_ERR_INVALID, "null pointer");
+  hipStream_t s;
+  NXEC_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return NXEC_OK;
+}
+int nxec_stream_destroy(void *stream) {
+  NXEC_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_stream_sync(void *stream) {
+  NXEC_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_device_sync(void) {
+  NXEC_HIP(hipDeviceSynchronize());
+  return NXEC_OK;
+}
+int nxec_event_create(void **event) {
+  if (!event) return set_error(NXEC_ERR_INVALID, "null pointer");
+  hipEvent_t ev;
+  NXEC_HIP(hipEventCreate(&ev));
+  *event = ev;
+  return NXEC_OK;
+}
+int nxec_event_destroy(void *event) {
+  NXEC_HIP(hipEventDestroy(static_cast<hipEvent_t>(event)));
+  return NXEC_OK;
+}
+int nxec_event_record(void *event, void *stream) {
+  NXEC_HIP(hipEventRecord(static_cast<hipEvent_t>(event), static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_event_elapsed_ms(void *start, void *stop, float *ms) {
+  if (!ms) return set_error(NXEC_ERR_INVALID, "null pointer");
+  NXEC_HIP(hipEventSynchronize(static_cast<hipEvent_t>(stop)));
+  NXEC_HIP(hipEventElapsedTime(ms, static_cast<hipEvent_t>(start), static_cast<hipEvent_t>(stop)));
+  return NXEC_OK;
+}
+int nxec_fill_random(void *d_dst, size_t bytes, uint64_t seed, void *stream) {
+  return launch_fill(d_dst, bytes, seed, stream);
+}
+int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream) {
+  if (!out) return set_error(NXEC_ERR_INVALID, "null pointer");
+  uint64_t *d_acc = nullptr;
+  NXEC_HIP(hipMalloc(reinterpret_cast<void **>(&d_acc), sizeof(uint64_t)));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipError_t e = hipMemsetAsync(d_acc, 0, sizeof(uint64_t), st);
+  int rc = e == hipSuccess ? launch_checksum(d_src, bytes, d_acc, st) : hip_err(e, "hipMemsetAsync");
+  if (rc == NXEC_OK) {
+    e = hipMemcpyAsync(out, d_acc, sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = hip_err(e, "checksum readback");
+  }
+  (void)hipFree(d_acc);
+  return rc;
+}
+
+int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len) {
+  if (!ctx || !buf || buf_len <= 0 || k < 1 || k > NXEC_MAX_K)
+    return set_error(NXEC_ERR_INVALID, "invalid arguments");
+  LaunchInfo li = plan_launch(k, len / 16, nstripes, ctx->num_cus, false);
+  std::snprintf(buf, buf_len,
+                "{\"kernel\":\"%s\",\"k\":%d,\"rows\":%d,\"passes\":%d,\"lds_copies\":%d,\"block\":%d,\"grid\":%d,"
+                "\"lds_bytes\":%d,\"cus\":%d}",
+                li.variant, k, rows, (rows + kMaxRowsPerPass - 1) / kMaxRowsPerPass, li.lds_copies, li.block, li.grid,
+                li.lds_bytes, ctx->num_cus);
+  return NXEC_OK;
+}
+
+}  // extern "C"

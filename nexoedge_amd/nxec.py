@@ -1,0 +1,293 @@
+"""Python view of the C ABI (include/nxec.h) for tests, benchmarks and tools.
+
+Everything here is plumbing around libnxec: device buffers, contexts and the
+RS entry points.  The coding arithmetic itself only exists in the gfx950
+kernels; host-side helpers below are the planning math (matrices), which the
+reference also runs on the host (rs.cc:26,196,219,290,316).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from ._lib import NXEC_OK, NxecError, check, lib
+
+
+def _u8(a: np.ndarray) -> C.c_void_p:
+    assert a.dtype == np.uint8 and a.flags["C_CONTIGUOUS"]
+    return C.c_void_p(a.ctypes.data)
+
+
+def _i32(v: Optional[Iterable[int]]):
+    if v is None:
+        return None, None
+    arr = np.ascontiguousarray(np.asarray(list(v), dtype=np.int32))
+    return arr, C.c_void_p(arr.ctypes.data)
+
+
+# ---------------------------------------------------------------- host math
+def gf_mul(a: int, b: int) -> int:
+    return int(lib.nxec_gf_mul(a, b))
+
+
+def gf_inv(a: int) -> int:
+    return int(lib.nxec_gf_inv(a))
+
+
+def gen_rs_matrix(n: int, k: int) -> np.ndarray:
+    """ISA-L gf_gen_rs_matrix (rs.cc:26): n x k, identity on top."""
+    a = np.zeros((n, k), dtype=np.uint8)
+    lib.nxec_gf_gen_rs_matrix(_u8(a), n, k)
+    return a
+
+
+def invert_matrix(m: np.ndarray) -> Optional[np.ndarray]:
+    src = np.ascontiguousarray(m, dtype=np.uint8).copy()
+    n = src.shape[0]
+    out = np.zeros((n, n), dtype=np.uint8)
+    rc = lib.nxec_gf_invert_matrix(_u8(src), _u8(out), n)
+    return None if rc != 0 else out
+
+
+def init_tables(coeffs: np.ndarray) -> np.ndarray:
+    c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    rows, k = c.shape
+    out = np.zeros(rows * k * 32, dtype=np.uint8)
+    lib.nxec_ec_init_tables(k, rows, _u8(c), _u8(out))
+    return out
+
+
+def rs_plan(n: int, k: int, failed: Sequence[int], is_repair: bool):
+    """RSCode::preDecode (rs.cc:238-322) -> (input_ids, min_inputs, repair_matrix|None)."""
+    f, fp = _i32(failed)
+    ids = np.zeros(n, dtype=np.int32)
+    ni, mi = C.c_int(0), C.c_int(0)
+    rm = np.zeros((max(len(failed), 1), k), dtype=np.uint8)
+    rc = lib.nxec_rs_plan(n, k, fp, len(failed), 1 if is_repair else 0, C.c_void_p(ids.ctypes.data), C.byref(ni),
+                          C.byref(mi), _u8(rm))
+    check(rc, "nxec_rs_plan")
+    return ids[: ni.value].tolist(), mi.value, (rm[: len(failed)] if is_repair else None)
+
+
+def decode_matrix(n: int, k: int, input_ids: Sequence[int], targets: Sequence[int]) -> np.ndarray:
+    a, ap = _i32(input_ids)
+    t, tp = _i32(targets)
+    out = np.zeros((max(len(targets), 1), k), dtype=np.uint8)
+    check(lib.nxec_rs_decode_matrix(n, k, ap, tp, len(targets), _u8(out)), "nxec_rs_decode_matrix")
+    return out[: len(targets)]
+
+
+# ------------------------------------------------------- host-buffer encode
+def encode_host(coeffs: np.ndarray, data: Sequence[np.ndarray]) -> list:
+    """CodingUtils::encode / ec_encode_data on host buffers (GPU-executed)."""
+    c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    rows, k = c.shape
+    n = len(data[0]) if data else 0
+    ins = [np.ascontiguousarray(d, dtype=np.uint8) for d in data]
+    outs = [np.zeros(n, dtype=np.uint8) for _ in range(rows)]
+    inp = (C.c_void_p * k)(*[d.ctypes.data for d in ins])
+    outp = (C.c_void_p * rows)(*[o.ctypes.data for o in outs])
+    check(lib.nxec_encode_host(n, k, rows, _u8(c), inp, outp), "nxec_encode_host")
+    return outs
+
+
+def ec_encode_data(gftbls: np.ndarray, k: int, rows: int, data: Sequence[np.ndarray]) -> list:
+    """Drop-in ISA-L signature: coefficients come from 32-byte tables."""
+    t = np.ascontiguousarray(gftbls, dtype=np.uint8)
+    n = len(data[0])
+    ins = [np.ascontiguousarray(d, dtype=np.uint8) for d in data]
+    outs = [np.zeros(n, dtype=np.uint8) for _ in range(rows)]
+    inp = (C.c_void_p * k)(*[d.ctypes.data for d in ins])
+    outp = (C.c_void_p * rows)(*[o.ctypes.data for o in outs])
+    check(lib.nxec_ec_encode_data_status(n, k, rows, _u8(t), inp, outp), "nxec_ec_encode_data")
+    return outs
+
+
+# ------------------------------------------------------------- device side
+def device_count() -> int:
+    c = C.c_int(0)
+    rc = lib.nxec_device_count(C.byref(c))
+    return c.value if rc == NXEC_OK else 0
+
+
+def device_info(dev: int = 0) -> dict:
+    name = C.create_string_buffer(64)
+    cus = C.c_int(0)
+    mem = C.c_int64(0)
+    check(lib.nxec_device_info(dev, name, 64, C.byref(cus), C.byref(mem)), "nxec_device_info")
+    return {"arch": name.value.decode(), "cus": cus.value, "mem": mem.value}
+
+
+def device_sync() -> None:
+    check(lib.nxec_device_sync(), "nxec_device_sync")
+
+
+class DeviceBuffer:
+    """Raw device allocation (hipMalloc) with host copy helpers."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = C.c_void_p()
+        check(lib.nxec_dev_malloc(C.byref(p), max(self.nbytes, 1)), "nxec_dev_malloc")
+        self.ptr = p.value
+
+    def __int__(self):
+        return self.ptr
+
+    def addr(self, offset: int = 0) -> C.c_void_p:
+        return C.c_void_p(self.ptr + offset)
+
+    def upload(self, arr: np.ndarray, offset: int = 0, stream=None) -> None:
+        a = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        assert offset + a.nbytes <= self.nbytes
+        check(lib.nxec_memcpy_h2d(self.addr(offset), C.c_void_p(a.ctypes.data), a.nbytes, stream), "h2d")
+        check(lib.nxec_stream_sync(stream), "sync")
+
+    def download(self, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(n, dtype=np.uint8)
+        check(lib.nxec_memcpy_d2h(C.c_void_p(out.ctypes.data), self.addr(offset), n, stream), "d2h")
+        check(lib.nxec_stream_sync(stream), "sync")
+        return out
+
+    def fill_random(self, seed: int, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> None:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        check(lib.nxec_fill_random(self.addr(offset), n, C.c_uint64(seed), stream), "fill")
+        check(lib.nxec_stream_sync(stream), "sync")
+
+    def memset(self, value: int, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> None:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        check(lib.nxec_memset(self.addr(offset), value, n, stream), "memset")
+        check(lib.nxec_stream_sync(stream), "sync")
+
+    def checksum(self, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> int:
+        n = self.nbytes - offset if nbytes is None else nbytes
+        out = C.c_uint64(0)
+        check(lib.nxec_checksum(self.addr(offset), n, C.byref(out), stream), "checksum")
+        return out.value
+
+    def free(self) -> None:
+        if self.ptr:
+            lib.nxec_dev_free(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class PinnedBuffer:
+    """hipHostMalloc'd host memory exposed as a numpy uint8 array."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib.nxec_host_malloc_pinned(C.byref(p), max(int(nbytes), 1)), "nxec_host_malloc_pinned")
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+        self.array = np.ctypeslib.as_array((C.c_ubyte * max(self.nbytes, 1)).from_address(self.ptr))[: self.nbytes]
+
+    def free(self) -> None:
+        if self.ptr:
+            self.array = None
+            lib.nxec_host_free_pinned(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+
+class Event:
+    def __init__(self):
+        p = C.c_void_p()
+        check(lib.nxec_event_create(C.byref(p)), "nxec_event_create")
+        self.ptr = p.value
+
+    def record(self, stream=None) -> None:
+        check(lib.nxec_event_record(C.c_void_p(self.ptr), stream), "nxec_event_record")
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = C.c_float(0)
+        check(lib.nxec_event_elapsed_ms(C.c_void_p(self.ptr), C.c_void_p(end.ptr), C.byref(ms)), "elapsed")
+        return float(ms.value)
+
+
+class Context:
+    """An nxec_ctx_t bound to one device: stream + staging pools."""
+
+    def __init__(self, device: int = 0):
+        p = C.c_void_p()
+        check(lib.nxec_ctx_create(device, C.byref(p)), "nxec_ctx_create")
+        self.ptr = p.value
+        self.device = device
+
+    @property
+    def stream(self) -> C.c_void_p:
+        return C.c_void_p(lib.nxec_ctx_stream(C.c_void_p(self.ptr)))
+
+    def sync(self) -> None:
+        check(lib.nxec_stream_sync(self.stream), "nxec_stream_sync")
+
+    def stripes_mul(self, coeffs: np.ndarray, src: int, dst: int, *, src_idx=None, dst_idx=None, copy_idx=None,
+                    src_chunk_stride: int, src_stripe_stride: int, dst_chunk_stride: int, dst_stripe_stride: int,
+                    length: int, nstripes: int, stream=None) -> None:
+        c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+        rows, k = c.shape
+        si, sip = _i32(src_idx)
+        di, dip = _i32(dst_idx)
+        ci, cip = _i32(copy_idx)
+        rc = lib.nxec_stripes_mul(C.c_void_p(self.ptr), rows, k, _u8(c), C.c_void_p(int(src)), sip,
+                                  src_chunk_stride, src_stripe_stride, C.c_void_p(int(dst)), dip, dst_chunk_stride,
+                                  dst_stripe_stride, cip, length, nstripes, stream)
+        check(rc, "nxec_stripes_mul")
+
+    def stripes_mul_ptrs(self, coeffs: np.ndarray, src_ptrs: int, dst_ptrs: int, length: int, nstripes: int,
+                         stream=None) -> None:
+        c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+        rows, k = c.shape
+        rc = lib.nxec_stripes_mul_ptrs(C.c_void_p(self.ptr), rows, k, _u8(c), C.c_void_p(int(src_ptrs)),
+                                       C.c_void_p(int(dst_ptrs)), length, nstripes, stream)
+        check(rc, "nxec_stripes_mul_ptrs")
+
+    def rs_encode(self, n: int, k: int, stripes: int, chunk_stride: int, stripe_stride: int, length: int,
+                  nstripes: int, stream=None) -> None:
+        check(lib.nxec_rs_encode_stripes(C.c_void_p(self.ptr), n, k, C.c_void_p(int(stripes)), chunk_stride,
+                                         stripe_stride, length, nstripes, stream), "nxec_rs_encode_stripes")
+
+    def rs_recover(self, n: int, k: int, failed: Sequence[int], stripes: int, chunk_stride: int,
+                   stripe_stride: int, length: int, nstripes: int, stream=None) -> None:
+        f, fp = _i32(failed)
+        check(lib.nxec_rs_recover_stripes(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(stripes)),
+                                          chunk_stride, stripe_stride, length, nstripes, stream),
+              "nxec_rs_recover_stripes")
+
+    def rs_decode(self, n: int, k: int, failed: Sequence[int], stripes: int, chunk_stride: int, stripe_stride: int,
+                  out: int, out_chunk_stride: int, out_stripe_stride: int, length: int, nstripes: int,
+                  stream=None) -> None:
+        f, fp = _i32(failed)
+        check(lib.nxec_rs_decode_stripes(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(stripes)),
+                                         chunk_stride, stripe_stride, C.c_void_p(int(out)), out_chunk_stride,
+                                         out_stripe_stride, length, nstripes, stream), "nxec_rs_decode_stripes")
+
+    def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
+                             batch_stripes: int = 0) -> None:
+        check(lib.nxec_rs_encode_host_batch(C.c_void_p(self.ptr), n, k, C.c_void_p(int(h_data)),
+                                            C.c_void_p(int(h_parity)), length, nstripes, batch_stripes),
+              "nxec_rs_encode_host_batch")
+
+    def describe_launch(self, rows: int, k: int, length: int, nstripes: int) -> str:
+        buf = C.create_string_buffer(512)
+        check(lib.nxec_describe_launch(C.c_void_p(self.ptr), rows, k, length, nstripes, buf, 512), "describe")
+        return buf.value.decode()
+
+    def close(self) -> None:
+        if self.ptr:
+            lib.nxec_ctx_destroy(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+
+__all__ = [
+    "NxecError", "gf_mul", "gf_inv", "gen_rs_matrix", "invert_matrix", "init_tables", "rs_plan", "decode_matrix",
+    "encode_host", "ec_encode_data", "device_count", "device_info", "device_sync", "DeviceBuffer", "PinnedBuffer",
+    "Event", "Context",
+]

@@ -1,0 +1,68 @@
+"""The C-ABI library loads, exports every symbol include/nxec.h declares, and
+fails loudly (no CPU fallback) when no GPU is visible.  CPU only."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import nexoedge_amd
+from nexoedge_amd import _lib, nxec
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "nxec.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nxec_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_isal_replacements():
+    syms = declared_symbols()
+    for s in ("nxec_ec_encode_data", "nxec_ec_init_tables", "nxec_gf_gen_rs_matrix", "nxec_gf_invert_matrix",
+              "nxec_gf_mul", "nxec_stripes_mul", "nxec_rs_encode_stripes", "nxec_rs_recover_stripes",
+              "nxec_rs_decode_stripes"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    missing = [s for s in declared_symbols() if not hasattr(_lib.lib, s)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (nxec_\w+)", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_python_binding_covers_header():
+    assert set(declared_symbols()) <= set(_lib.EXPORTED)
+
+
+def test_library_is_gfx950_code():
+    # the offload bundle inside the .so names its target triple
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_version():
+    assert "gfx950" in nexoedge_amd.__version__
+
+
+@pytest.mark.skipif(nxec.device_count() > 0, reason="a GPU is visible")
+def test_no_device_fails_loudly():
+    with pytest.raises(nxec.NxecError) as e:
+        nxec.Context(0)
+    assert e.value.code == _lib.NXEC_ERR_NODEV
+    import numpy as np
+    with pytest.raises(nxec.NxecError):
+        nxec.encode_host(np.ones((1, 2), dtype=np.uint8), [np.zeros(16, np.uint8)] * 2)
+
+
+def test_invalid_arguments_rejected_before_device_use():
+    # argument validation happens before any device work
+    rc = _lib.lib.nxec_stripes_mul(None, 1, 2, None, None, None, 0, 0, None, None, 0, 0, None, 16, 1, None)
+    assert rc == _lib.NXEC_ERR_INVALID
+    rc = _lib.lib.nxec_rs_encode_stripes(None, 3, 4, None, 0, 0, 16, 1, None)
+    assert rc == _lib.NXEC_ERR_INVALID
+    assert b"invalid" in _lib.lib.nxec_last_error()

@@ -1,0 +1,73 @@
+"""libnxec's host planning math (section 1 and rs_plan of include/nxec.h)
+against the reference's golden vectors.  These are host-side matrix routines
+(no GPU), exactly like rs.cc:26,196,219,290,316 run on the host."""
+import numpy as np
+
+from nexoedge_amd import nxec
+from helpers import hexbytes
+
+
+def test_gf_mul_and_inv(golden):
+    mt = np.array([[nxec.gf_mul(a, b) for b in range(256)] for a in range(256)], dtype=np.uint8)
+    import hashlib
+    assert hashlib.sha256(mt.tobytes()).hexdigest() == golden["gf_mul_table_sha256"]
+    inv = np.array([nxec.gf_inv(a) for a in range(256)], dtype=np.uint8)
+    assert np.array_equal(inv, hexbytes(golden["gf_inv_hex"]))
+
+
+def test_gen_rs_matrix(golden):
+    for m in golden["matrices"]:
+        assert nxec.gen_rs_matrix(m["n"], m["k"]).tobytes().hex() == m["hex"]
+
+
+def test_init_tables(golden):
+    for t in golden["init_tables"]:
+        n, k = t["n"], t["k"]
+        assert nxec.init_tables(nxec.gen_rs_matrix(n, k)[k:]).tobytes().hex() == t["hex"]
+
+
+def test_invert(golden):
+    for t in golden["inverses"]:
+        n, k = t["n"], t["k"]
+        inv = nxec.invert_matrix(nxec.gen_rs_matrix(n, k)[t["rows"]])
+        assert inv is not None and inv.tobytes().hex() == t["inv_hex"]
+    assert nxec.invert_matrix(np.zeros((3, 3), dtype=np.uint8)) is None
+
+
+def test_plan_matches_reference_repair_matrices(golden):
+    for c in golden["repair"]:
+        n, k, f = c["n"], c["k"], c["failed"]
+        ids, mi, rm = nxec.rs_plan(n, k, f, True)
+        assert len(ids) == c["ninputs"] and mi == k
+        assert rm.tobytes().hex() == c["repair_matrix_hex"], (n, k, f)
+
+
+def test_plan_read_inputs(golden):
+    for c in golden["decode"]:
+        ids, mi, _ = nxec.rs_plan(c["n"], c["k"], c["failed"], False)
+        assert len(ids) == c["ninputs"] and mi == c["k"]
+        assert not set(ids) & set(c["failed"]) and ids == sorted(ids)
+
+
+def test_plan_rejects_too_many_failures():
+    import pytest
+    with pytest.raises(nxec.NxecError):
+        nxec.rs_plan(6, 4, [0, 1, 2], False)
+
+
+def test_decode_matrix_rows_are_consistent():
+    # data targets -> inverse rows; parity targets -> enc row x inverse
+    n, k = 14, 10
+    enc = nxec.gen_rs_matrix(n, k)
+    ids = [1, 2, 3, 5, 6, 7, 8, 9, 10, 12]
+    m = nxec.decode_matrix(n, k, ids, [0, 4, 11, 13])
+    inv = nxec.invert_matrix(enc[ids])
+    assert np.array_equal(m[0], inv[0]) and np.array_equal(m[1], inv[4])
+    for row, t in ((2, 11), (3, 13)):
+        want = np.zeros(k, dtype=np.uint8)
+        for j in range(k):
+            s = 0
+            for l in range(k):
+                s ^= nxec.gf_mul(int(inv[l, j]), int(enc[t, l]))
+            want[j] = s
+        assert np.array_equal(m[row], want)
