@@ -15,7 +15,12 @@ LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hi
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(wildcard $(CSRC)/coding/*.hh)
 
-all: $(LIBDIR)/libnxec.so oracle/liboracle.so
+all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test
+
+# C++ surface test (reference coding_test.cc flows through RSCode on the GPU)
+build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p $(dir $@)
@@ -28,6 +33,13 @@ $(LIBDIR)/libnxec.so: $(LIB_OBJS)
 oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_oracle.h
 	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c -o $@ -lpthread
 
+# design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
+tune: tools/microbench/tune_mul tools/microbench/lut_variants
+tools/microbench/tune_mul: tools/microbench/tune_mul.hip $(LIBDIR)/libnxec.so
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
+tools/microbench/lut_variants: tools/microbench/lut_variants.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
+
 ref:
 	bash oracle/build_ref.sh
 
@@ -37,4 +49,4 @@ golden: ref
 clean:
 	rm -rf build $(LIBDIR)/libnxec.so oracle/liboracle.so
 
-.PHONY: all ref golden clean
+.PHONY: all ref golden clean tune

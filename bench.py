@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 import nexoedge_amd  # noqa: E402  (load libnxec before torch: one HIP runtime)
 from nexoedge_amd import nxec  # noqa: E402
+from nexoedge_amd.dist import RankGroup  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PATTERNS = ([0, 1, 2, 3], [10, 11, 12, 13], [1, 4, 11, 13])
@@ -48,45 +49,6 @@ def parse():
     ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D->encode->D2H pipeline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
     return ap.parse_args()
-
-
-def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        pg = dist
-    return world, rank, local, pg
-
-
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
-
-
-def max_over_ranks(pg, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(pg, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
 
 
 def cpu_baseline(args, n, k, cs):
@@ -158,7 +120,8 @@ def load_traffic(path, launch_bytes):
 
 def main():
     args = parse()
-    world, rank, local, pg = dist_setup(args)
+    grp = RankGroup()
+    world, rank, local = grp.world, grp.rank, grp.local_rank
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
     p = n - k
     e = len(PATTERNS[0])
@@ -188,7 +151,7 @@ def main():
     nxec.device_sync()
 
     evs = [[nxec.Event() for _ in range(3)] for _ in range(args.steps)]
-    barrier(pg)
+    grp.barrier()
     nxec.device_sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -196,15 +159,15 @@ def main():
     ctx.sync()
     nxec.device_sync()
     t1 = time.perf_counter()
-    barrier(pg)
+    grp.barrier()
     local_s = t1 - t0
-    elapsed = max_over_ranks(pg, local_s)
+    elapsed = grp.max(local_s)
 
     enc_ms = [evs[i][0].elapsed_ms(evs[i][1]) for i in range(args.steps)]
     dec_ms = [evs[i][1].elapsed_ms(evs[i][2]) for i in range(args.steps)]
     enc_avg = sum(enc_ms) / len(enc_ms)
     dec_avg = sum(dec_ms) / len(dec_ms)
-    total_bytes = sum_over_ranks(pg, float(step_bytes * args.steps))
+    total_bytes = grp.sum(float(step_bytes * args.steps))
 
     result = None
     if rank == 0:
@@ -250,7 +213,7 @@ def main():
                 "decode_frac": round(dec_gbs / HBM_PEAK_GBS, 4),
                 "decode_avg_launch_ms": round(dec_avg, 4),
             },
-            "user_data_gib_s": round(sum_over_ranks(None, 2 * ns * k * cs * args.steps * world) / elapsed / GIB, 2),
+            "user_data_gib_s": round(2 * ns * k * cs * args.steps * world / elapsed / GIB, 2),
         }
     if args.host_inclusive and rank == 0:
         result["host_inclusive"] = host_inclusive(ctx, n, k, cs)
@@ -260,8 +223,7 @@ def main():
         print(json.dumps(result), flush=True)
     buf.free()
     ctx.close()
-    if pg is not None:
-        pg.destroy_process_group()
+    grp.close()
 
 
 def host_inclusive(ctx, n, k, cs, ns=512):

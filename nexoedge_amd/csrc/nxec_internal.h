@@ -16,6 +16,7 @@ int repair_rows(int n, int k, const std::vector<uint8_t> &enc, const int32_t *in
                 int ntargets, uint8_t *out);
 
 constexpr int kMaxRowsPerPass = 4;  // one packed 32-bit LDS entry holds 4 row products
+constexpr uint32_t kNoCopy = 0xFFFFFFFFu;
 
 // Kernel arguments of one GF(2^8) stripe-multiply pass (<= 4 output rows).
 // Chunk (s, c) of the source lives at src + s*src_stripe_stride + c*src_chunk_stride
@@ -28,16 +29,19 @@ struct MulArgs {
   int64_t src_chunk_stride, src_stripe_stride;
   int64_t dst_chunk_stride, dst_stripe_stride;
   int64_t len;         // bytes per chunk
-  int64_t vec_count;   // 16-byte vectors per chunk handled by the vector kernel
+  int64_t vec_begin;   // first 16-byte vector (per chunk) of this vector-kernel launch
+  int64_t vec_count;   // 16-byte vectors per chunk handled by this vector-kernel launch
   int64_t byte_begin;  // first byte handled by the byte kernel
   int64_t nstripes;
   int32_t k, rows;
   int32_t any_copy;                 // copy_idx has entries >= 0
   int32_t dst_ptr_row0;             // gather mode: first row of this pass inside dst_ptrs[s*rows_total + r]
   int32_t dst_ptr_rows;             // gather mode: rows_total
-  int16_t src_idx[NXEC_MAX_K + 1];
-  int16_t dst_idx[kMaxRowsPerPass];
-  int16_t copy_idx[NXEC_MAX_K + 1];  // -1 = none
+  // strided form: byte offsets of the chunks inside a stripe (idx * chunk_stride,
+  // precomputed on the host; < 4 GiB so they stay single 32-bit SGPRs)
+  uint32_t src_off[NXEC_MAX_K + 1];
+  uint32_t dst_off[kMaxRowsPerPass];
+  uint32_t copy_off[NXEC_MAX_K + 1];  // kNoCopy = none
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // row-major rows x k
 };
 
@@ -50,7 +54,7 @@ struct LaunchInfo {
 };
 
 // Chooses and describes the vector-kernel launch for (k, len, nstripes).
-LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool gather);
+LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool tunable);
 // Enqueues one pass (vector kernel + byte kernel for tails / misaligned data).
 int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).

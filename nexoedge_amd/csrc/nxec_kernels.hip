@@ -42,6 +42,22 @@ namespace {
 constexpr int kBlock = 1024;       // threads per workgroup (16 waves)
 constexpr int kMaxTemplK = 20;     // k with a fully unrolled kernel; larger k use the dynamic kernel
 constexpr int kLdsBytes = 160 * 1024;
+// next-tile prefetch doubles the source registers (4*K VGPRs); beyond these k
+// the 128-VGPR budget of a 1024-thread workgroup would spill
+constexpr int kPrefetchMaxK = 10;
+constexpr int kPrefetchMaxKCopy = 8;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Streaming (nontemporal) 16-byte accesses: every source byte is read once and
+// every parity byte written once, so keep them from displacing the tables'
+// neighbours in L2/MALL.  Measured +2-3 % at RS(10,4) 1 MiB (tools/microbench/tune_mul.hip).
+__device__ __forceinline__ u32x4 ld_stream(const uint8_t *p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+}
+__device__ __forceinline__ void st_stream(uint8_t *p, u32x4 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
+}
 
 __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -72,13 +88,13 @@ __device__ __forceinline__ void build_tables(const MulArgs &a, int k, uint32_t *
 template <bool GATHER>
 __device__ __forceinline__ uint8_t *dst_row(const MulArgs &a, uint32_t s, int r) {
   if (GATHER) return a.dst_ptrs[static_cast<size_t>(s) * a.dst_ptr_rows + a.dst_ptr_row0 + r];
-  return a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + a.dst_idx[r] * a.dst_chunk_stride;
+  return a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + a.dst_off[r];
 }
 
 template <bool GATHER>
 __device__ __forceinline__ const uint8_t *src_chunk(const MulArgs &a, uint32_t s, int j) {
   if (GATHER) return a.src_ptrs[static_cast<size_t>(s) * a.k + j];
-  return a.src + static_cast<int64_t>(s) * a.src_stripe_stride + a.src_idx[j] * a.src_chunk_stride;
+  return a.src + static_cast<int64_t>(s) * a.src_stripe_stride + a.src_off[j];
 }
 
 // acc[p] holds the 4 row products of column byte p (p = 4q + b); write row r's
@@ -100,12 +116,12 @@ __device__ __forceinline__ void store_rows(const MulArgs &a, uint32_t s, uint32_
   }
 #pragma unroll
   for (int r = 0; r < kMaxRowsPerPass; r++) {
-    if (r < a.rows) reinterpret_cast<uint4 *>(dst_row<GATHER>(a, s, r))[v] = make_uint4(o[r][0], o[r][1], o[r][2], o[r][3]);
+    if (r < a.rows) st_stream(dst_row<GATHER>(a, s, r) + static_cast<size_t>(v) * 16, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
   }
 }
 
 template <int R>
-__device__ __forceinline__ void lookup16(const char *tb, const uint4 d, uint32_t acc[16]) {
+__device__ __forceinline__ void lookup16(const char *tb, const u32x4 d, uint32_t acc[16]) {
   const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -117,9 +133,57 @@ __device__ __forceinline__ void lookup16(const char *tb, const uint4 d, uint32_t
   }
 }
 
-// Fully unrolled vector kernel: all K source loads of a column vector in flight.
-template <int K, int R, bool GATHER>
+// Column vector v (relative to the launch's vec_begin) of stripe s for tile t;
+// tiles are kBlock consecutive vectors of one stripe.
+struct TilePos {
+  uint32_t s, v;
+};
+__device__ __forceinline__ TilePos tile_pos(uint32_t t, uint32_t tps) {
+  const uint32_t s = t / tps;
+  return {s, (t - s * tps) * kBlock + threadIdx.x};
+}
+
+// FULL: every tile is complete (vec_count % kBlock == 0), so no lane predicate
+// and no exec-mask regions around the loads; the ragged remainder of a chunk
+// gets its own predicated launch.
+template <int K, bool GATHER, bool FULL>
+__device__ __forceinline__ void load_tile(const MulArgs &a, TilePos p, uint32_t nvec, u32x4 (&d)[K]) {
+  if (FULL || p.v < nvec) {
+    const size_t off = (static_cast<size_t>(a.vec_begin) + p.v) * 16;
+#pragma unroll
+    for (int j = 0; j < K; j++) d[j] = ld_stream(src_chunk<GATHER>(a, p.s, j) + off);
+  }
+}
+
+// Lookups + parity stores (+ optional pass-through copies) of one tile.
+template <int K, int R, bool GATHER, bool COPY, bool FULL>
+__device__ __forceinline__ void compute_tile(const MulArgs &a, TilePos p, uint32_t nvec, const char *tlane,
+                                             const u32x4 (&d)[K]) {
+  if (!FULL && p.v >= nvec) return;
+  const uint32_t vg = static_cast<uint32_t>(a.vec_begin) + p.v;
+  uint32_t acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+  for (int j = 0; j < K; j++) lookup16<R>(tlane + j * 1024 * R, d[j], acc);
+  store_rows<GATHER>(a, p.s, vg, acc);
+  if (COPY) {
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const uint32_t c = a.copy_off[j];
+      if (c != kNoCopy)
+        st_stream(a.dst + static_cast<int64_t>(p.s) * a.dst_stripe_stride + c + static_cast<size_t>(vg) * 16, d[j]);
+    }
+  }
+}
+
+// Fully unrolled vector kernel: all K source loads of a column vector in
+// flight, and (PF) the next tile's loads issued before this tile's lookups.
+// COPY: fused pass-through of sources (full-output decode); a separate
+// instantiation so encode/recover kernels carry no copy-address registers.
+template <int K, int R, bool GATHER, bool COPY, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
+  constexpr bool PF = K <= ((COPY || !FULL) ? kPrefetchMaxKCopy : kPrefetchMaxK);
   extern __shared__ uint32_t tab[];
   build_tables<R>(a, K, tab);
   __syncthreads();
@@ -127,27 +191,27 @@ __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
   const uint32_t tps = (nvec + kBlock - 1) / kBlock;
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
   const char *tlane = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
-  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint32_t s = t / tps;
-    const uint32_t v = (t - s * tps) * kBlock + threadIdx.x;
-    if (v >= nvec) continue;
-    uint4 d[K];
+  if constexpr (PF) {
+    uint32_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    u32x4 d[K];
+    load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d);
+    for (; t < ntiles; t += gridDim.x) {
+      const uint32_t tn = t + gridDim.x;
+      u32x4 nx[K];
+      if (tn < ntiles) load_tile<K, GATHER, FULL>(a, tile_pos(tn, tps), nvec, nx);
+      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, d);
+      if (tn < ntiles) {
 #pragma unroll
-    for (int j = 0; j < K; j++) d[j] = reinterpret_cast<const uint4 *>(src_chunk<GATHER>(a, s, j))[v];
-    uint32_t acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) acc[i] = 0;
-#pragma unroll
-    for (int j = 0; j < K; j++) lookup16<R>(tlane + j * 1024 * R, d[j], acc);
-    store_rows<GATHER>(a, s, v, acc);
-    if (!GATHER && a.any_copy) {
-#pragma unroll
-      for (int j = 0; j < K; j++) {
-        const int c = a.copy_idx[j];
-        if (c >= 0)
-          reinterpret_cast<uint4 *>(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride)[v] =
-              d[j];
+        for (int j = 0; j < K; j++) d[j] = nx[j];
       }
+    }
+  } else {
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      u32x4 d[K];
+      const TilePos p = tile_pos(t, tps);
+      load_tile<K, GATHER, FULL>(a, p, nvec, d);
+      compute_tile<K, R, GATHER, COPY, FULL>(a, p, nvec, tlane, d);
     }
   }
 }
@@ -165,24 +229,24 @@ __global__ __launch_bounds__(kBlock) void k_mul_vec_dyn(const MulArgs a) {
   const char *tl = reinterpret_cast<const char *>(tab);
   for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const uint32_t s = t / tps;
-    const uint32_t v = (t - s * tps) * kBlock + threadIdx.x;
-    if (v >= nvec) continue;
+    const uint32_t vl = (t - s * tps) * kBlock + threadIdx.x;
+    if (vl >= nvec) continue;
+    const uint32_t v = static_cast<uint32_t>(a.vec_begin) + vl;
     uint32_t acc[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) acc[i] = 0;
     for (int j0 = 0; j0 < k; j0 += 4) {
-      uint4 d[4];
+      u32x4 d[4];
 #pragma unroll
       for (int jj = 0; jj < 4; jj++)
-        if (j0 + jj < k) d[jj] = reinterpret_cast<const uint4 *>(src_chunk<GATHER>(a, s, j0 + jj))[v];
+        if (j0 + jj < k) d[jj] = ld_stream(src_chunk<GATHER>(a, s, j0 + jj) + static_cast<size_t>(v) * 16);
 #pragma unroll
       for (int jj = 0; jj < 4; jj++) {
         if (j0 + jj < k) {
           lookup16<1>(tl + (j0 + jj) * 1024, d[jj], acc);
-          const int c = a.copy_idx[j0 + jj];
-          if (!GATHER && a.any_copy && c >= 0)
-            reinterpret_cast<uint4 *>(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride)[v] =
-                d[jj];
+          const uint32_t c = a.copy_off[j0 + jj];
+          if (!GATHER && a.any_copy && c != kNoCopy)
+            st_stream(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c + static_cast<size_t>(v) * 16, d[jj]);
         }
       }
     }
@@ -207,8 +271,8 @@ __global__ __launch_bounds__(256) void k_mul_bytes(const MulArgs a) {
     for (int j = 0; j < k; j++) {
       const uint8_t x = src_chunk<GATHER>(a, s, j)[pos];
       acc ^= tab[j * 256 + x];
-      const int c = a.copy_idx[j];
-      if (!GATHER && a.any_copy && c >= 0) a.dst[static_cast<int64_t>(s) * a.dst_stripe_stride + c * a.dst_chunk_stride + pos] = x;
+      const uint32_t c = a.copy_off[j];
+      if (!GATHER && a.any_copy && c != kNoCopy) a.dst[static_cast<int64_t>(s) * a.dst_stripe_stride + c + pos] = x;
     }
     for (int r = 0; r < a.rows; r++) dst_row<GATHER>(a, s, r)[pos] = static_cast<uint8_t>(acc >> (8 * r));
   }
@@ -251,49 +315,66 @@ __global__ void k_checksum(const uint8_t *p, int64_t bytes, unsigned long long *
 
 using KernelFn = void (*)(MulArgs);
 
-template <int R, bool G, int... Ks>
+template <int R, bool G, bool CP, bool FULL, int... Ks>
 constexpr std::array<KernelFn, sizeof...(Ks)> vec_table(std::integer_sequence<int, Ks...>) {
-  return {{&k_mul_vec<Ks + 1, R, G>...}};
+  return {{&k_mul_vec<Ks + 1, R, G, CP, FULL>...}};
 }
 
-// strided form: every (k, R) for tuning; gather form: the default R only
-const auto kVecR16 = vec_table<16, false>(std::make_integer_sequence<int, 10>{});        // k = 1..10
-const auto kVecR8 = vec_table<8, false>(std::make_integer_sequence<int, kMaxTemplK>{});  // k = 1..20
-const auto kVecR1 = vec_table<1, false>(std::make_integer_sequence<int, kMaxTemplK>{});  // k = 1..20
-const auto kVecG16 = vec_table<16, true>(std::make_integer_sequence<int, 10>{});         // k = 1..10
-const auto kVecG8 = vec_table<8, true>(std::make_integer_sequence<int, kMaxTemplK>{});   // k = 1..20
+// One table per (form, R, full-tiles): indexed by k-1.  Strided full-tile
+// kernels exist for every R (tuning knob NXEC_LDS_R); every other form only
+// at the default R (16 for k <= 10, else 8).
+using KTable = std::array<KernelFn, kMaxTemplK>;
+template <int R, bool G, bool CP, bool FULL>
+KTable make_table() {
+  KTable t{};
+  if constexpr (R == 16) {
+    auto a = vec_table<16, G, CP, FULL>(std::make_integer_sequence<int, 10>{});
+    for (int i = 0; i < 10; i++) t[i] = a[i];
+  } else {
+    auto a = vec_table<R, G, CP, FULL>(std::make_integer_sequence<int, kMaxTemplK>{});
+    for (int i = 0; i < kMaxTemplK; i++) t[i] = a[i];
+  }
+  return t;
+}
+// [gather][copy][full]
+const KTable kDefR16[2][2][2] = {
+    {{make_table<16, false, false, false>(), make_table<16, false, false, true>()},
+     {make_table<16, false, true, false>(), make_table<16, false, true, true>()}},
+    {{make_table<16, true, false, false>(), make_table<16, true, false, true>()}, {KTable{}, KTable{}}}};
+const KTable kDefR8[2][2][2] = {
+    {{make_table<8, false, false, false>(), make_table<8, false, false, true>()},
+     {make_table<8, false, true, false>(), make_table<8, false, true, true>()}},
+    {{make_table<8, true, false, false>(), make_table<8, true, false, true>()}, {KTable{}, KTable{}}}};
+const KTable kTuneR1 = make_table<1, false, false, true>();
 
 int hip_fail(hipError_t e, const char *what) {
   return set_error(NXEC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
 // LDS replication policy (NXEC_LDS_R=1|8|16 overrides, for tuning only).
-int choose_r(int k) {
-  const char *env = std::getenv("NXEC_LDS_R");
-  int want = env ? std::atoi(env) : 0;
+int choose_r(int k, bool tunable) {
   if (k > kMaxTemplK) return 1;
+  const char *env = tunable ? std::getenv("NXEC_LDS_R") : nullptr;
+  const int want = env ? std::atoi(env) : 0;
   if (want == 1) return 1;
   if (want == 8) return 8;
-  if (want == 16 && k <= 10) return 16;
   return k <= 10 ? 16 : 8;
 }
 
-KernelFn vec_kernel(int k, int r, bool gather) {
+KernelFn vec_kernel(int k, int r, bool gather, bool copy, bool full) {
   if (k > kMaxTemplK) return gather ? &k_mul_vec_dyn<true> : &k_mul_vec_dyn<false>;
-  if (gather) return k <= 10 ? kVecG16[k - 1] : kVecG8[k - 1];
-  if (r == 16) return kVecR16[k - 1];
-  if (r == 8) return kVecR8[k - 1];
-  return kVecR1[k - 1];
+  if (r == 1 && !gather && !copy && full) return kTuneR1[k - 1];
+  if (r == 16 && k <= 10) return kDefR16[gather][copy][full][k - 1];
+  return kDefR8[gather][copy][full][k - 1];
 }
 
-// gather kernels always use the default replication
-int gather_r(int k) { return k > kMaxTemplK ? 1 : (k <= 10 ? 16 : 8); }
+int default_r(int k) { return choose_r(k, false); }
 
 }  // namespace
 
-LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool gather) {
+LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool tunable) {
   LaunchInfo li{};
-  li.lds_copies = gather ? gather_r(k) : choose_r(k);
+  li.lds_copies = choose_r(k, tunable);
   li.block = kBlock;
   li.lds_bytes = k * 1024 * li.lds_copies;
   int per_cu = kLdsBytes / (li.lds_bytes > 0 ? li.lds_bytes : 1);
@@ -313,13 +394,17 @@ int prepare_kernels() {
     return hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   };
   for (int k = 1; k <= kMaxTemplK; k++) {
-    for (int r : {1, 8, 16}) {
-      if (r == 16 && k > 10) continue;
-      hipError_t e = raise(vec_kernel(k, r, false), k * 1024 * r);
-      if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec)");
-    }
-    hipError_t e = raise(vec_kernel(k, gather_r(k), true), k * 1024 * gather_r(k));
-    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec gather)");
+    for (int g = 0; g < 2; g++)
+      for (int c = 0; c < 2; c++)
+        for (int f = 0; f < 2; f++) {
+          if (g && c) continue;
+          const int r = default_r(k);
+          hipError_t e = raise(vec_kernel(k, r, g, c, f), k * 1024 * r);
+          if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec)");
+        }
+    hipError_t e = raise(kTuneR1[k - 1], k * 1024);
+    if (e == hipSuccess) e = raise(kDefR8[0][0][1][k - 1], k * 1024 * 8);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec tune)");
   }
   for (KernelFn fn : {&k_mul_vec_dyn<false>, &k_mul_vec_dyn<true>, &k_mul_bytes<false>, &k_mul_bytes<true>}) {
     hipError_t e = raise(fn, NXEC_MAX_K * 1024);
@@ -336,11 +421,22 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
     if (tps * a.nstripes >= (int64_t(1) << 32) || a.vec_count >= (int64_t(1) << 32))
       return set_error(NXEC_ERR_INVALID, "batch too large for one launch (split nstripes)");
     const bool gather = a.src_ptrs != nullptr;
-    LaunchInfo li = plan_launch(a.k, a.vec_count, a.nstripes, num_cus, gather);
-    KernelFn fn = vec_kernel(a.k, li.lds_copies, gather);
-    hipLaunchKernelGGL(fn, dim3(li.grid), dim3(li.block), li.lds_bytes, st, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "launch k_mul_vec");
+    const bool copy = a.any_copy != 0;
+    // complete tiles first (no lane predicates), then the ragged remainder
+    const int64_t full = a.vec_count / kBlock * kBlock;
+    const int64_t parts[2][2] = {{0, full}, {full, a.vec_count - full}};
+    for (int pi = 0; pi < 2; pi++) {
+      if (parts[pi][1] <= 0) continue;
+      MulArgs b = a;
+      b.vec_begin = a.vec_begin + parts[pi][0];
+      b.vec_count = parts[pi][1];
+      const bool is_full = pi == 0;
+      LaunchInfo li = plan_launch(b.k, b.vec_count, b.nstripes, num_cus, !gather && !copy && is_full);
+      KernelFn fn = vec_kernel(b.k, li.lds_copies, gather, copy, is_full);
+      hipLaunchKernelGGL(fn, dim3(li.grid), dim3(li.block), li.lds_bytes, st, b);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return hip_fail(e, "launch k_mul_vec");
+    }
   }
   if (a.byte_begin < a.len) {
     const int64_t total = (a.len - a.byte_begin) * a.nstripes;

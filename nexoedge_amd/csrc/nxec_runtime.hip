@@ -195,15 +195,24 @@ int stripes_mul_impl(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coef
   a.nstripes = nstripes;
   a.k = k;
   a.dst_ptr_rows = rows;
-  for (int j = 0; j < k; j++) {
-    const int32_t si = src_idx ? src_idx[j] : j;
-    if (si < 0 || si > 32767) return set_error(NXEC_ERR_INVALID, "src_idx[%d]=%d out of range", j, si);
-    a.src_idx[j] = static_cast<int16_t>(si);
-    const int32_t ci = copy_idx ? copy_idx[j] : -1;
-    if (ci > 32767) return set_error(NXEC_ERR_INVALID, "copy_idx[%d]=%d out of range", j, ci);
-    a.copy_idx[j] = static_cast<int16_t>(ci < 0 ? -1 : ci);
-  }
   if (gather && any_copy) return set_error(NXEC_ERR_INVALID, "copy_idx is only supported in the strided form");
+  // chunk byte offsets inside a stripe (kept 32-bit for the kernels' scalar address math)
+  auto chunk_off = [&](int32_t idx, int64_t stride, uint32_t *out) -> bool {
+    if (idx < 0) return false;
+    const int64_t off = static_cast<int64_t>(idx) * stride;
+    if (stride < 0 || off + len > (int64_t(1) << 32) - 1) return false;
+    *out = static_cast<uint32_t>(off);
+    return true;
+  };
+  for (int j = 0; j < k && !gather; j++) {
+    const int32_t si = src_idx ? src_idx[j] : j;
+    if (!chunk_off(si, src_cs, &a.src_off[j]))
+      return set_error(NXEC_ERR_INVALID, "src_idx[%d]=%d: offset out of range (chunks of a stripe must lie within 4 GiB)",
+                       j, si);
+    a.copy_off[j] = kNoCopy;
+    if (copy_idx && copy_idx[j] >= 0 && !chunk_off(copy_idx[j], dst_cs, &a.copy_off[j]))
+      return set_error(NXEC_ERR_INVALID, "copy_idx[%d]=%d: offset out of range", j, copy_idx[j]);
+  }
 
   bool vec_ok = true;
   if (!gather) {
@@ -228,12 +237,12 @@ int stripes_mul_impl(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coef
     a.dst_ptr_row0 = r0;
     for (int r = 0; r < kMaxRowsPerPass; r++) {
       const int rr = r0 + r;
-      int32_t di = 0;
-      if (r < pr) {
-        di = dst_idx ? dst_idx[rr] : rr;
-        if (di < 0 || di > 32767) return set_error(NXEC_ERR_INVALID, "dst_idx[%d]=%d out of range", rr, di);
+      a.dst_off[r] = 0;
+      if (r < pr && !gather) {
+        const int32_t di = dst_idx ? dst_idx[rr] : rr;
+        if (!chunk_off(di, dst_cs, &a.dst_off[r]))
+          return set_error(NXEC_ERR_INVALID, "dst_idx[%d]=%d: offset out of range", rr, di);
       }
-      a.dst_idx[r] = static_cast<int16_t>(di);
       for (int j = 0; j < k; j++) a.coef[r * k + j] = r < pr ? coeffs[static_cast<size_t>(rr) * k + j] : 0;
     }
     for (int64_t s0 = 0; s0 < nstripes; s0 += max_stripes) {
@@ -638,7 +647,7 @@ int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream) 
 int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len) {
   if (!ctx || !buf || buf_len <= 0 || k < 1 || k > NXEC_MAX_K)
     return set_error(NXEC_ERR_INVALID, "invalid arguments");
-  LaunchInfo li = plan_launch(k, len / 16, nstripes, ctx->num_cus, false);
+  LaunchInfo li = plan_launch(k, len / 16, nstripes, ctx->num_cus, true);
   std::snprintf(buf, buf_len,
                 "{\"kernel\":\"%s\",\"k\":%d,\"rows\":%d,\"passes\":%d,\"lds_copies\":%d,\"block\":%d,\"grid\":%d,"
                 "\"lds_bytes\":%d,\"cus\":%d}",

@@ -1,0 +1,69 @@
+"""Multi-rank path on CPU: stripe sharding covers every stripe exactly once and
+the benchmark's barrier / max-over-ranks reduction works under gloo with
+world_size 2 (the N>1 bench path, without a GPU)."""
+import os
+import socket
+import subprocess
+import sys
+
+from nexoedge_amd.dist import shard_range
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_shard_range_partitions():
+    for total in (0, 1, 7, 4096, 4097, 10**6 + 3):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                lo, hi = shard_range(total, r, world)
+                assert 0 <= lo <= hi <= total
+                seen.extend(range(lo, hi)) if total < 10000 else seen.append((lo, hi))
+            if total < 10000:
+                assert seen == list(range(total))
+            else:
+                assert seen[0][0] == 0 and seen[-1][1] == total
+                assert all(a[1] == b[0] for a, b in zip(seen, seen[1:]))
+            sizes = [hi - lo for lo, hi in (shard_range(total, r, world) for r in range(world))]
+            assert max(sizes) - min(sizes) <= 1
+
+
+WORKER = r"""
+import os, sys, time
+sys.path.insert(0, {root!r})
+from nexoedge_amd.dist import RankGroup, shard_range
+g = RankGroup()
+lo, hi = shard_range(4096, g.rank, g.world)
+g.barrier()
+t = 0.010 * (g.rank + 1)          # pretend rank r took (r+1)*10 ms
+mx = g.max(t)
+tot = g.sum(hi - lo)
+print(f"rank={{g.rank}} world={{g.world}} lo={{lo}} hi={{hi}} max={{mx:.3f}} total={{tot:.0f}}", flush=True)
+g.close()
+"""
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gloo_world2_reduction(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(WORKER.format(root=ROOT))
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=180) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    lines = sorted(l for o, _ in outs for l in o.splitlines() if l.startswith("rank="))
+    assert lines[0] == "rank=0 world=2 lo=0 hi=2048 max=0.020 total=4096"
+    assert lines[1] == "rank=1 world=2 lo=2048 hi=4096 max=0.020 total=4096"
