@@ -15,7 +15,12 @@ LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hi
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(wildcard $(CSRC)/coding/*.hh)
 
-all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test
+all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test
+
+# rs.cc's ISA-L call sequence compiled against include/nxec_isal_compat.h (plain C)
+build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h $(LIBDIR)/libnxec.so
+	@mkdir -p build
+	gcc -std=c11 -O2 -Wall -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
 
 # C++ surface test (reference coding_test.cc flows through RSCode on the GPU)
 build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)

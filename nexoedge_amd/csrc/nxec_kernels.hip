@@ -192,19 +192,28 @@ __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
   const char *tlane = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
   if constexpr (PF) {
+    // ping-pong register buffers, manually unrolled x2: the next tile's loads
+    // are issued (and pinned there by sched_barrier) before this tile's
+    // lookups, and no register copies force a vmcnt(0) at the loop head.  The
+    // last prefetch re-reads the current tile instead of branching, so the
+    // waitcnt pass sees the same count of in-flight loads on every path.
     uint32_t t = blockIdx.x;
     if (t >= ntiles) return;
-    u32x4 d[K];
-    load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d);
-    for (; t < ntiles; t += gridDim.x) {
-      const uint32_t tn = t + gridDim.x;
-      u32x4 nx[K];
-      if (tn < ntiles) load_tile<K, GATHER, FULL>(a, tile_pos(tn, tps), nvec, nx);
-      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, d);
-      if (tn < ntiles) {
-#pragma unroll
-        for (int j = 0; j < K; j++) d[j] = nx[j];
-      }
+    u32x4 A[K], B[K];
+    load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
+    while (true) {
+      const uint32_t tb = t + gridDim.x;
+      load_tile<K, GATHER, FULL>(a, tile_pos(tb < ntiles ? tb : t, tps), nvec, B);
+      __builtin_amdgcn_sched_barrier(0);
+      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, A);
+      if (tb >= ntiles) break;
+      t = tb;
+      const uint32_t ta = t + gridDim.x;
+      load_tile<K, GATHER, FULL>(a, tile_pos(ta < ntiles ? ta : t, tps), nvec, A);
+      __builtin_amdgcn_sched_barrier(0);
+      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, B);
+      if (ta >= ntiles) break;
+      t = ta;
     }
   } else {
     for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {

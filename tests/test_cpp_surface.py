@@ -65,3 +65,23 @@ def test_rscode_surface_matches_reference(golden):
     # 2 CAR modes x (54 coding_test pairs + 3 config geometries)
     assert checked["ENC"] == 2 * 57 and checked["DEC"] == 2 * 57
     assert checked["REP"] > 500 and checked["RP2"] > 2000
+
+
+COMPAT = os.path.join(ROOT, "build", "isal_compat_test")
+
+
+def test_compat_binary_built():
+    assert os.path.exists(COMPAT), "run `make` (build/isal_compat_test)"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,cs", [(14, 10, 1000), (6, 4, 31), (20, 16, 4096), (16, 12, 65537), (4, 2, 1)])
+def test_isal_compat_header_drop_in(golden, n, k, cs):
+    """rs.cc's ISA-L call sequence, recompiled against nxec_isal_compat.h, gives
+    the reference's parity and restores the data."""
+    r = subprocess.run([COMPAT, str(n), str(k), str(cs)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = dict(l.split(" ", 1) for l in r.stdout.splitlines() if " " in l)
+    want = [c["parity_sha256"] for c in golden["encode"] if (c["n"], c["k"], c["cs"]) == (n, k, cs)]
+    assert want and lines["PARITY"].strip() == want[0]
+    assert lines["DECODED"].strip() == sha(fill_bytes(k * cs, case_seed(n, k, cs)))
