@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--cpu-stripes", type=int, default=192)
     ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D->encode->D2H pipeline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--workload", choices=["rs10_4", "repair12", "mixed16"], default="rs10_4",
+                    help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
+    ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
+    ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
     return ap.parse_args()
 
 
@@ -118,39 +122,134 @@ def load_traffic(path, launch_bytes):
         return None
 
 
+class Workload:
+    """One bench step = the ops in `ops`, each (label, fn(step_index), algorithmic bytes)."""
+
+    def __init__(self, name, metric, config, ops, buffers, roof_kernel, stripes):
+        self.name, self.metric, self.config, self.ops = name, metric, config, ops
+        self.buffers, self.roof_kernel, self.stripes = buffers, roof_kernel, stripes
+
+
+def wl_rs10_4(args, ctx, stream, rank):
+    """Configs 2+3: RS(10,4) encode + 4-erasure recover, 1 MiB chunks, 4096 stripes."""
+    n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
+    p, e, stripe = n - k, len(PATTERNS[0]), n * cs
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(0xC0FFEE + rank * 7919)  # synthetic data; parity region overwritten by encode
+    ops = [
+        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream), ns * (k + p) * cs),
+        ("decode", lambda i: ctx.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], buf.ptr, cs, stripe, cs, ns, stream),
+         ns * (k + e) * cs),
+    ]
+    config = {
+        "workload": f"RS(10,4) (n,k)=({n},{k}) encode + {e}-erasure recover, {cs >> 10} KiB chunks, "
+                    f"{ns}-stripe batch per GPU, [stripe][chunk][byte] in HBM",
+        "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": PATTERNS,
+        "byte_accounting": "encode (k+p)*cs + decode (k+e)*cs per stripe (ISA-L erasure_code_perf.c)",
+        "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
+    }
+    return Workload("rs10_4", "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident", config, ops, [buf],
+                    f"k_mul_vec<K={k},R=16> (encode launch)", ns)
+
+
+def wl_repair12(args, ctx, stream, rank):
+    """Config 4: RS(12,4) single-failure repair; fused (k+1) recover and the
+    unfused agent partial-encode path (racks of 4 chunks: partial 1 x g encodes,
+    container_manager.cc:251, then the CAR XOR finalize, rs.cc:94-109)."""
+    import numpy as np
+
+    n, k, cs, ns, g = 16, 12, args.chunk, args.stripes, 4
+    stripe = n * cs
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(0xBEEF + rank)
+    ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream)
+    failed = args.failed if args.failed is not None else 0
+    ids, _, rm = nxec.rs_plan(n, k, [failed], True)
+    ids = ids[:k]
+    groups = []  # (start index in ids, size) per rack
+    j = 0
+    while j < k:
+        rack, st = ids[j] // g, j
+        while j < k and ids[j] // g == rack:
+            j += 1
+        groups.append((st, j - st))
+    G = len(groups)
+    part = nxec.DeviceBuffer(ns * G * cs)
+    ones = np.ones((1, G), dtype=np.uint8)
+
+    def unfused(i):
+        for gi, (st, sz) in enumerate(groups):
+            ctx.stripes_mul(rm[:, st:st + sz], buf.ptr, part.ptr, src_idx=ids[st:st + sz], dst_idx=[gi],
+                            src_chunk_stride=cs, src_stripe_stride=stripe, dst_chunk_stride=cs,
+                            dst_stripe_stride=G * cs, length=cs, nstripes=ns, stream=stream)
+        ctx.stripes_mul(ones, part.ptr, buf.ptr, dst_idx=[failed], src_chunk_stride=cs, src_stripe_stride=G * cs,
+                        dst_chunk_stride=cs, dst_stripe_stride=stripe, length=cs, nstripes=ns, stream=stream)
+
+    ops = [
+        ("repair_fused", lambda i: ctx.rs_recover(n, k, [failed], buf.ptr, cs, stripe, cs, ns, stream),
+         ns * (k + 1) * cs),
+        ("repair_car_unfused", unfused, ns * (k + 1 + 2 * G) * cs),
+    ]
+    config = {"workload": f"RS(12,4) (n,k)=(16,12) single-failure repair of chunk {failed}, racks of {g} chunks "
+                          f"({G} partials), {cs >> 10} KiB chunks, {ns} stripes per GPU",
+              "stripes_per_gpu": ns, "chunk_bytes": cs,
+              "byte_accounting": "fused (k+1)*cs; CAR unfused (k+1+2G)*cs per stripe (SURVEY 8d)",
+              "launch": json.loads(ctx.describe_launch(1, k, cs, ns))}
+    return Workload("repair12", "GiB/s RS(12,4) single-failure repair, 1 MiB chunks, device-resident", config, ops,
+                    [buf, part], "k_mul_vec<K=12,R=8> (fused recover, rows=1)", ns)
+
+
+def wl_mixed16(args, ctx, stream, rank):
+    """Config 5: RS(16,4) alternating encode / 4-erasure decode at one chunk size;
+    the stripe count fills ~args.gib GiB per GPU."""
+    n, k, cs = 20, 16, args.chunk
+    stripe = n * cs
+    ns = max(1, int(args.gib * (1 << 30)) // stripe)
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(0xFACE + rank)
+    pats = ([0, 1, 2, 3], [16, 17, 18, 19], [1, 4, 17, 19])
+    ops = [
+        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream), ns * n * cs),
+        ("decode", lambda i: ctx.rs_recover(n, k, pats[i % 3], buf.ptr, cs, stripe, cs, ns, stream), ns * n * cs),
+    ]
+    config = {"workload": f"RS(16,4) (n,k)=(20,16) encode + 4-erasure recover, {cs >> 10} KiB chunks, {ns} stripes "
+                          f"(~{args.gib} GiB) per GPU",
+              "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": pats,
+              "launch": json.loads(ctx.describe_launch(4, k, cs, ns))}
+    return Workload("mixed16", f"GiB/s RS(16,4) encode+decode, {cs >> 10} KiB chunks, device-resident", config, ops,
+                    [buf], "k_mul_vec<K=16,R=8> (encode launch)", ns)
+
+
+WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16}
+
+
 def main():
     args = parse()
     grp = RankGroup()
     world, rank, local = grp.world, grp.rank, grp.local_rank
-    n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
-    p = n - k
-    e = len(PATTERNS[0])
     ctx = nxec.Context(local)
     stream = ctx.stream
-    stripe = n * cs
-    buf = nxec.DeviceBuffer(ns * stripe)
-    buf.fill_random(0xC0FFEE + rank * 7919)  # synthetic data; parity region overwritten by encode
-
-    enc_bytes = ns * (k + p) * cs
-    dec_bytes = ns * (k + e) * cs
-    step_bytes = enc_bytes + dec_bytes
+    wl = WORKLOADS[args.workload](args, ctx, stream, rank)
+    step_bytes = sum(b for _, _, b in wl.ops)
+    nops = len(wl.ops)
 
     def step(i, evs=None):
+        for oi, (_, fn, _) in enumerate(wl.ops):
+            if evs is not None:
+                evs[oi].record(stream)
+            fn(i)
         if evs is not None:
-            evs[0].record(stream)
-        ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream)
-        if evs is not None:
-            evs[1].record(stream)
-        ctx.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], buf.ptr, cs, stripe, cs, ns, stream)
-        if evs is not None:
-            evs[2].record(stream)
+            evs[nops].record(stream)
 
-    for i in range(args.warmup):
+    for i in range(max(1, args.warmup)):
         step(i)
     ctx.sync()
     nxec.device_sync()
+    # every op is idempotent on a consistent batch (re-encode / recover rewrite
+    # the same bytes), so the batch checksum must not change across the timed steps
+    sum_before = wl.buffers[0].checksum()
 
-    evs = [[nxec.Event() for _ in range(3)] for _ in range(args.steps)]
+    evs = [[nxec.Event() for _ in range(nops + 1)] for _ in range(args.steps)]
     grp.barrier()
     nxec.device_sync()
     t0 = time.perf_counter()
@@ -160,24 +259,21 @@ def main():
     nxec.device_sync()
     t1 = time.perf_counter()
     grp.barrier()
-    local_s = t1 - t0
-    elapsed = grp.max(local_s)
-
-    enc_ms = [evs[i][0].elapsed_ms(evs[i][1]) for i in range(args.steps)]
-    dec_ms = [evs[i][1].elapsed_ms(evs[i][2]) for i in range(args.steps)]
-    enc_avg = sum(enc_ms) / len(enc_ms)
-    dec_avg = sum(dec_ms) / len(dec_ms)
+    elapsed = grp.max(t1 - t0)
     total_bytes = grp.sum(float(step_bytes * args.steps))
+    verified = grp.sum(0.0 if wl.buffers[0].checksum() == sum_before else 1.0) == 0.0
+
+    # per-op event-timed durations on the launch stream
+    op_ms = [sum(evs[i][oi].elapsed_ms(evs[i][oi + 1]) for i in range(args.steps)) / args.steps for oi in range(nops)]
 
     result = None
     if rank == 0:
-        # roofline of the dominant kernel (k_mul_vec<10, R16>, encode launch):
-        # algorithmic bytes per launch / event-timed launch duration
-        enc_gbs = enc_bytes / (enc_avg * 1e-3) / 1e9
-        dec_gbs = dec_bytes / (dec_avg * 1e-3) / 1e9
-        traffic = load_traffic(args.pmc_summary, enc_bytes)
+        # roofline of the dominant kernel: algorithmic bytes per launch / event-timed launch duration
+        b0 = wl.ops[0][2]
+        gbs0 = b0 / (op_ms[0] * 1e-3) / 1e9
+        traffic = load_traffic(args.pmc_summary, b0) if wl.name == "rs10_4" else None
         result = {
-            "metric": "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident",
+            "metric": wl.metric,
             "value": round(total_bytes / elapsed / GIB, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -189,39 +285,34 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes, device-generated)",
-            "config": {
-                "workload": f"RS(10,4) (n,k)=({n},{k}) encode + {e}-erasure recover, {cs >> 10} KiB chunks, "
-                            f"{ns}-stripe batch per GPU, [stripe][chunk][byte] in HBM",
-                "stripes_per_gpu": ns,
-                "chunk_bytes": cs,
-                "erasure_patterns": PATTERNS,
-                "byte_accounting": "encode (k+p)*cs + decode (k+e)*cs per stripe (ISA-L erasure_code_perf.c)",
-                "parallelism": f"stripe-sharded x{world}, no collectives",
-                "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
-            },
+            "verified": verified,
+            "config": dict(wl.config, parallelism=f"stripe-sharded x{world}, no collectives"),
             "roofline": {
                 "bound": "hbm",
-                "achieved": round(enc_gbs, 1),
+                "achieved": round(gbs0, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(enc_gbs / HBM_PEAK_GBS, 4),
+                "frac": round(gbs0 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_mul_vec<K=10,R=16> (encode launch)",
-                "bytes_per_launch": enc_bytes,
-                "avg_launch_ms": round(enc_avg, 4),
-                "decode_achieved": round(dec_gbs, 1),
-                "decode_frac": round(dec_gbs / HBM_PEAK_GBS, 4),
-                "decode_avg_launch_ms": round(dec_avg, 4),
+                "kernel": wl.roof_kernel,
+                "bytes_per_launch": b0,
+                "avg_launch_ms": round(op_ms[0], 4),
             },
-            "user_data_gib_s": round(2 * ns * k * cs * args.steps * world / elapsed / GIB, 2),
+            "ops": {name: {"avg_ms": round(ms, 4), "bytes": b, "GB_s": round(b / (ms * 1e-3) / 1e9, 1),
+                           "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                    for (name, _, b), ms in zip(wl.ops, op_ms)},
         }
+        if wl.name == "rs10_4":
+            k, cs = args.k, args.chunk
+            result["user_data_gib_s"] = round(2 * wl.stripes * k * cs * args.steps * world / elapsed / GIB, 2)
     if args.host_inclusive and rank == 0:
-        result["host_inclusive"] = host_inclusive(ctx, n, k, cs)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, n, k, cs)
+        result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.name == "rs10_4":
+        result["cpu_baseline"] = cpu_baseline(args, args.n, args.k, args.chunk)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    buf.free()
+    for b in wl.buffers:
+        b.free()
     ctx.close()
     grp.close()
 

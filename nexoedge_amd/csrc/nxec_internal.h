@@ -47,6 +47,7 @@ struct MulArgs {
 
 struct LaunchInfo {
   const char *variant;
+  bool perm;        // VALU nibble-table kernel (single-row passes)
   int lds_copies;   // R: table replication factor
   int block;        // threads per workgroup
   int grid;         // workgroups
@@ -54,7 +55,8 @@ struct LaunchInfo {
 };
 
 // Chooses and describes the vector-kernel launch for (k, len, nstripes).
-LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool tunable);
+LaunchInfo plan_launch(int k, int rows, int64_t vec_count, int64_t nstripes, int num_cus, bool full, bool copy,
+                       bool gather);
 // Enqueues one pass (vector kernel + byte kernel for tails / misaligned data).
 int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).

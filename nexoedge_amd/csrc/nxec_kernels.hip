@@ -46,6 +46,8 @@ constexpr int kLdsBytes = 160 * 1024;
 // the 128-VGPR budget of a 1024-thread workgroup would spill
 constexpr int kPrefetchMaxK = 10;
 constexpr int kPrefetchMaxKCopy = 8;
+constexpr int kPermPrefetchMaxK = 4;
+constexpr int kPermMaxK = 13;  // beyond this the single-row VALU kernel would spill (128-VGPR budget)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -155,74 +157,163 @@ __device__ __forceinline__ void load_tile(const MulArgs &a, TilePos p, uint32_t 
   }
 }
 
-// Lookups + parity stores (+ optional pass-through copies) of one tile.
-template <int K, int R, bool GATHER, bool COPY, bool FULL>
-__device__ __forceinline__ void compute_tile(const MulArgs &a, TilePos p, uint32_t nvec, const char *tlane,
-                                             const u32x4 (&d)[K]) {
-  if (!FULL && p.v >= nvec) return;
-  const uint32_t vg = static_cast<uint32_t>(a.vec_begin) + p.v;
-  uint32_t acc[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) acc[i] = 0;
-#pragma unroll
-  for (int j = 0; j < K; j++) lookup16<R>(tlane + j * 1024 * R, d[j], acc);
-  store_rows<GATHER>(a, p.s, vg, acc);
+template <int K, bool COPY>
+__device__ __forceinline__ void copy_through(const MulArgs &a, uint32_t s, uint32_t vg, const u32x4 (&d)[K]) {
   if (COPY) {
 #pragma unroll
     for (int j = 0; j < K; j++) {
       const uint32_t c = a.copy_off[j];
       if (c != kNoCopy)
-        st_stream(a.dst + static_cast<int64_t>(p.s) * a.dst_stripe_stride + c + static_cast<size_t>(vg) * 16, d[j]);
+        st_stream(a.dst + static_cast<int64_t>(s) * a.dst_stripe_stride + c + static_cast<size_t>(vg) * 16, d[j]);
     }
   }
 }
 
-// Fully unrolled vector kernel: all K source loads of a column vector in
-// flight, and (PF) the next tile's loads issued before this tile's lookups.
-// COPY: fused pass-through of sources (full-output decode); a separate
-// instantiation so encode/recover kernels carry no copy-address registers.
-template <int K, int R, bool GATHER, bool COPY, bool FULL>
-__global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
-  constexpr bool PF = K <= ((COPY || !FULL) ? kPrefetchMaxKCopy : kPrefetchMaxK);
-  extern __shared__ uint32_t tab[];
-  build_tables<R>(a, K, tab);
-  __syncthreads();
+// --- algorithm 1: LDS product tables (any rows <= 4) ---
+template <int K, int R, bool GATHER, bool COPY>
+struct LdsBody {
+  static constexpr int kLds = K * 1024 * R;
+  static __device__ __forceinline__ void setup(const MulArgs &a, uint32_t *tab) { build_tables<R>(a, K, tab); }
+  const char *tlane;
+  __device__ explicit LdsBody(const uint32_t *tab)
+      : tlane(reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4) {}
+  __device__ __forceinline__ void operator()(const MulArgs &a, uint32_t s, uint32_t vg, const u32x4 (&d)[K]) const {
+    uint32_t acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++) lookup16<R>(tlane + j * 1024 * R, d[j], acc);
+    store_rows<GATHER>(a, s, vg, acc);
+    copy_through<K, COPY>(a, s, vg, d);
+  }
+};
+
+// --- algorithm 2: VALU nibble tables via v_perm_b32 (rows == 1) ---
+// c*x = c*(x & 15) ^ c*(x & 0xf0).  v_perm_b32 picks 4 bytes at once from an
+// 8-byte pool; a 16-entry nibble table is two pools, chosen per byte by the
+// nibble's bit 3.  That bit becomes a 0x00/0xFF byte mask through v_perm's
+// sign-replication selectors (8..11 copy bit 7 of pool bytes 1,3,5,7), and
+// v_bfi_b32 merges the two halves.  No LDS traffic per byte (only 2 uniform
+// ds_read_b128 per source per tile for the 32-byte table), so a single-row
+// pass (repair, agent partial encode, CAR XOR) is not bound by LDS banks.
+// Measured k=12 rows=1: 0.678 of 8 TB/s vs 0.608 for the LDS tables
+// (tools/microbench/shape_ceiling.hip).
+__device__ __forceinline__ uint32_t perm_mul(const uint32_t *t, uint32_t nl, uint32_t nh, uint32_t ml, uint32_t mh) {
+  const uint32_t l0 = __builtin_amdgcn_perm(t[1], t[0], nl), l1 = __builtin_amdgcn_perm(t[3], t[2], nl);
+  const uint32_t h0 = __builtin_amdgcn_perm(t[5], t[4], nh), h1 = __builtin_amdgcn_perm(t[7], t[6], nh);
+  return ((ml & l1) | (~ml & l0)) ^ ((mh & h1) | (~mh & h0));
+}
+
+template <int K, bool GATHER, bool COPY>
+struct PermBody {
+  static constexpr int kLds = K * 32;
+  // table of source j: bytes [32j .. 32j+15] = c*n, [32j+16 .. 32j+31] = c*(n<<4)
+  static __device__ __forceinline__ void setup(const MulArgs &a, uint32_t *tab) {
+    uint8_t *tb = reinterpret_cast<uint8_t *>(tab);
+    for (int i = threadIdx.x; i < K * 16; i += blockDim.x) {
+      const int j = i >> 4, n = i & 15;
+      const uint32_t c = a.coef[j];
+      tb[32 * j + n] = static_cast<uint8_t>(gf_mul_dev(c, n));
+      tb[32 * j + 16 + n] = static_cast<uint8_t>(gf_mul_dev(c, n << 4));
+    }
+  }
+  const uint32_t *tab;
+  __device__ explicit PermBody(const uint32_t *t) : tab(t) {}
+  __device__ __forceinline__ void operator()(const MulArgs &a, uint32_t s, uint32_t vg, const u32x4 (&d)[K]) const {
+    // opaque zero: keeps the (uniform) table reads next to their use instead of
+    // hoisting K*8 registers out of the tile loop
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+    const uint32_t *tt = tab + z;
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      const uint32_t w[4] = {d[j].x, d[j].y, d[j].z, d[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t x = w[q], x4 = x << 4;
+        const uint32_t nl = x & 0x07070707u, nh = (x >> 4) & 0x07070707u;
+        const uint32_t ml = __builtin_amdgcn_perm(x4, x4 << 8, 0x0B090A08u);
+        const uint32_t mh = __builtin_amdgcn_perm(x, x << 8, 0x0B090A08u);
+        o[q] ^= perm_mul(tt + 8 * j, nl, nh, ml, mh);
+      }
+    }
+    st_stream(dst_row<GATHER>(a, s, 0) + static_cast<size_t>(vg) * 16, u32x4{o[0], o[1], o[2], o[3]});
+    copy_through<K, COPY>(a, s, vg, d);
+  }
+};
+
+// Persistent tile loop.  Workgroup b owns the contiguous tile run
+// [b*ntiles/G, (b+1)*ntiles/G): consecutive 16 KiB column tiles of the same
+// stripes, so each CU walks its own few stripes sequentially (page / DRAM-row
+// locality; +4% over interleaving tiles across workgroups at RS(10,4) 1 MiB,
+// tools/microbench/tune_mul.hip PF4 vs PF3).  With PF the next tile's loads
+// go out before this tile's compute through two ping-pong register buffers
+// (manual 2x unroll pinned by sched_barrier: no register copies, so the
+// waitcnt pass keeps the prefetch in flight); the final prefetch re-reads the
+// current tile instead of branching, so every path has the same loads in flight.
+template <int K, bool GATHER, bool FULL, bool PF, class Body>
+__device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body) {
   const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
   const uint32_t tps = (nvec + kBlock - 1) / kBlock;
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  const char *tlane = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
+  // readfirstlane: the tile index is wave-uniform; keep its math on the SALU
+  uint32_t t = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x) * ntiles) / gridDim.x));
+  const uint32_t tend = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x + 1) * ntiles) / gridDim.x));
+  if (t >= tend) return;
+  auto run = [&](uint32_t tt, const u32x4(&d)[K]) {
+    const TilePos p = tile_pos(tt, tps);
+    if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
+  };
   if constexpr (PF) {
-    // ping-pong register buffers, manually unrolled x2: the next tile's loads
-    // are issued (and pinned there by sched_barrier) before this tile's
-    // lookups, and no register copies force a vmcnt(0) at the loop head.  The
-    // last prefetch re-reads the current tile instead of branching, so the
-    // waitcnt pass sees the same count of in-flight loads on every path.
-    uint32_t t = blockIdx.x;
-    if (t >= ntiles) return;
     u32x4 A[K], B[K];
     load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
     while (true) {
-      const uint32_t tb = t + gridDim.x;
-      load_tile<K, GATHER, FULL>(a, tile_pos(tb < ntiles ? tb : t, tps), nvec, B);
+      const uint32_t tb = t + 1;
+      load_tile<K, GATHER, FULL>(a, tile_pos(tb < tend ? tb : t, tps), nvec, B);
       __builtin_amdgcn_sched_barrier(0);
-      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, A);
-      if (tb >= ntiles) break;
+      run(t, A);
+      if (tb >= tend) break;
       t = tb;
-      const uint32_t ta = t + gridDim.x;
-      load_tile<K, GATHER, FULL>(a, tile_pos(ta < ntiles ? ta : t, tps), nvec, A);
+      const uint32_t ta = t + 1;
+      load_tile<K, GATHER, FULL>(a, tile_pos(ta < tend ? ta : t, tps), nvec, A);
       __builtin_amdgcn_sched_barrier(0);
-      compute_tile<K, R, GATHER, COPY, FULL>(a, tile_pos(t, tps), nvec, tlane, B);
-      if (ta >= ntiles) break;
+      run(t, B);
+      if (ta >= tend) break;
       t = ta;
     }
   } else {
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    for (; t < tend; t++) {
       u32x4 d[K];
-      const TilePos p = tile_pos(t, tps);
-      load_tile<K, GATHER, FULL>(a, p, nvec, d);
-      compute_tile<K, R, GATHER, COPY, FULL>(a, p, nvec, tlane, d);
+      load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d);
+      run(t, d);
     }
   }
+}
+
+// Fully unrolled vector kernels: all K source loads of a column vector in
+// flight.  COPY: fused pass-through of sources (full-output decode); a
+// separate instantiation so encode/recover kernels carry no copy registers.
+template <int K, int R, bool GATHER, bool COPY, bool FULL>
+__global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
+  constexpr bool PF = K <= ((COPY || !FULL) ? kPrefetchMaxKCopy : kPrefetchMaxK);
+  using Body = LdsBody<K, R, GATHER, COPY>;
+  extern __shared__ uint32_t tab[];
+  Body::setup(a, tab);
+  __syncthreads();
+  tile_loop<K, GATHER, FULL, PF>(a, Body(tab));
+}
+
+template <int K, bool GATHER, bool COPY, bool FULL>
+__global__ __launch_bounds__(kBlock) void k_mul_perm(const MulArgs a) {
+  constexpr bool PF = K <= kPermPrefetchMaxK;
+  using Body = PermBody<K, GATHER, COPY>;
+  extern __shared__ uint32_t tab[];
+  Body::setup(a, tab);
+  __syncthreads();
+  tile_loop<K, GATHER, FULL, PF>(a, Body(tab));
 }
 
 // Runtime-k vector kernel (k > kMaxTemplK), R = 1 tables, sources in groups of 4.
@@ -236,7 +327,9 @@ __global__ __launch_bounds__(kBlock) void k_mul_vec_dyn(const MulArgs a) {
   const uint32_t tps = (nvec + kBlock - 1) / kBlock;
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
   const char *tl = reinterpret_cast<const char *>(tab);
-  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const uint32_t t0 = static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x) * ntiles) / gridDim.x);
+  const uint32_t t1 = static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x + 1) * ntiles) / gridDim.x);
+  for (uint32_t t = t0; t < t1; t++) {
     const uint32_t s = t / tps;
     const uint32_t vl = (t - s * tps) * kBlock + threadIdx.x;
     if (vl >= nvec) continue;
@@ -356,6 +449,14 @@ const KTable kDefR8[2][2][2] = {
     {{make_table<8, true, false, false>(), make_table<8, true, false, true>()}, {KTable{}, KTable{}}}};
 const KTable kTuneR1 = make_table<1, false, false, true>();
 
+template <bool G, int... Ks>
+constexpr std::array<KernelFn, sizeof...(Ks)> perm_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_mul_perm<Ks + 1, G, false, true>...}};
+}
+// single-row kernels (complete tiles, no pass-through), [gather][k-1]
+const std::array<KernelFn, kPermMaxK> kPerm[2] = {perm_table<false>(std::make_integer_sequence<int, kPermMaxK>{}),
+                                                  perm_table<true>(std::make_integer_sequence<int, kPermMaxK>{})};
+
 int hip_fail(hipError_t e, const char *what) {
   return set_error(NXEC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
@@ -381,20 +482,38 @@ int default_r(int k) { return choose_r(k, false); }
 
 }  // namespace
 
-LaunchInfo plan_launch(int k, int64_t vec_count, int64_t nstripes, int num_cus, bool tunable) {
+// single-row passes use the VALU nibble-table kernel (NXEC_ALGO=lds forces LDS, for A/B)
+bool use_perm(int k, int rows, bool full, bool copy, bool gather) {
+  if (rows != 1 || k > kPermMaxK || !full || copy) return false;
+  if (k == 11 && !gather) return false;  // this instantiation alone spills (hipcc 7.2 schedule); LDS tables instead
+  const char *env = std::getenv("NXEC_ALGO");
+  return !(env && std::strcmp(env, "lds") == 0);
+}
+
+LaunchInfo plan_launch(int k, int rows, int64_t vec_count, int64_t nstripes, int num_cus, bool full, bool copy,
+                       bool gather) {
+  const bool tunable = !gather && !copy && full;
   LaunchInfo li{};
-  li.lds_copies = choose_r(k, tunable);
   li.block = kBlock;
-  li.lds_bytes = k * 1024 * li.lds_copies;
-  int per_cu = kLdsBytes / (li.lds_bytes > 0 ? li.lds_bytes : 1);
-  if (per_cu > 2) per_cu = 2;  // 2 x 16 waves = the CU's 32-wave limit
-  if (per_cu < 1) per_cu = 1;
+  int per_cu = 1;
+  if (use_perm(k, rows, full, copy, gather)) {
+    li.perm = true;
+    li.lds_copies = 0;
+    li.lds_bytes = k * 32;
+    li.variant = "vec_perm";
+  } else {
+    li.lds_copies = choose_r(k, tunable);
+    li.lds_bytes = k * 1024 * li.lds_copies;
+    per_cu = kLdsBytes / (li.lds_bytes > 0 ? li.lds_bytes : 1);
+    if (per_cu > 2) per_cu = 2;  // 2 x 16 waves = the CU's 32-wave limit
+    if (per_cu < 1) per_cu = 1;
+    li.variant = k > kMaxTemplK ? "vec_dyn" : "vec_lds";
+  }
   const int64_t tps = (vec_count + kBlock - 1) / kBlock;
   int64_t ntiles = tps * nstripes;
   int64_t grid = static_cast<int64_t>(num_cus) * per_cu;
   if (grid > ntiles) grid = ntiles;
   li.grid = static_cast<int>(grid);
-  li.variant = k > kMaxTemplK ? "vec_dyn" : "vec_unrolled";
   return li;
 }
 
@@ -440,8 +559,8 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
       b.vec_begin = a.vec_begin + parts[pi][0];
       b.vec_count = parts[pi][1];
       const bool is_full = pi == 0;
-      LaunchInfo li = plan_launch(b.k, b.vec_count, b.nstripes, num_cus, !gather && !copy && is_full);
-      KernelFn fn = vec_kernel(b.k, li.lds_copies, gather, copy, is_full);
+      LaunchInfo li = plan_launch(b.k, b.rows, b.vec_count, b.nstripes, num_cus, is_full, copy, gather);
+      KernelFn fn = li.perm ? kPerm[gather][b.k - 1] : vec_kernel(b.k, li.lds_copies, gather, copy, is_full);
       hipLaunchKernelGGL(fn, dim3(li.grid), dim3(li.block), li.lds_bytes, st, b);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return hip_fail(e, "launch k_mul_vec");

@@ -647,7 +647,9 @@ int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream) 
 int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len) {
   if (!ctx || !buf || buf_len <= 0 || k < 1 || k > NXEC_MAX_K)
     return set_error(NXEC_ERR_INVALID, "invalid arguments");
-  LaunchInfo li = plan_launch(k, len / 16, nstripes, ctx->num_cus, true);
+  const int64_t nvec = len / 16;
+  LaunchInfo li = plan_launch(k, std::min(rows, static_cast<int>(kMaxRowsPerPass)), nvec, nstripes, ctx->num_cus,
+                              nvec % 1024 == 0, false, false);
   std::snprintf(buf, buf_len,
                 "{\"kernel\":\"%s\",\"k\":%d,\"rows\":%d,\"passes\":%d,\"lds_copies\":%d,\"block\":%d,\"grid\":%d,"
                 "\"lds_bytes\":%d,\"cus\":%d}",

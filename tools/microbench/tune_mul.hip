@@ -114,8 +114,17 @@ __global__ __launch_bounds__(NT) void k_tune(const Args a) {
   const int64_t sstride = static_cast<int64_t>(K + 4) * a.cstride;  // [stripe][k data][4 parity]
   uint32_t t = blockIdx.x;
   if (t >= ntiles) return;
-  if constexpr (PF == 3) {  // ping-pong buffers, manual 2x unroll: no register copies, no waits on the prefetch
+  if constexpr (PF >= 3) {  // ping-pong buffers, manual 2x unroll: no register copies, no waits on the prefetch
     static_assert(VPL == 1, "PF3 is VPL 1");
+    // PF 3: tiles interleaved over workgroups (t, t+grid, ...); PF 4: each
+    // workgroup owns a contiguous run of tiles (stays inside a few stripes)
+    uint32_t tend = ntiles, tstep = gridDim.x;
+    if (PF == 4) {
+      t = static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x) * ntiles) / gridDim.x);
+      tend = static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x + 1) * ntiles) / gridDim.x);
+      tstep = 1;
+      if (t >= tend) return;
+    }
     auto ld1 = [&](uint32_t tt, u32x4 (&dd)[K]) {
       const uint32_t s = tt / tps;
       const uint32_t off = (tt - s * tps) * tile_bytes + threadIdx.x * 16;
@@ -137,17 +146,17 @@ __global__ __launch_bounds__(NT) void k_tune(const Args a) {
     u32x4 A[K], B[K];
     ld1(t, A);
     while (true) {
-      uint32_t tb = t + gridDim.x;
-      ld1(tb < ntiles ? tb : t, B);
+      uint32_t tb = t + tstep;
+      ld1(tb < tend ? tb : t, B);
       __builtin_amdgcn_sched_barrier(0);
       comp(t, A);
-      if (tb >= ntiles) break;
+      if (tb >= tend) break;
       t = tb;
-      uint32_t ta = t + gridDim.x;
-      ld1(ta < ntiles ? ta : t, A);
+      uint32_t ta = t + tstep;
+      ld1(ta < tend ? ta : t, A);
       __builtin_amdgcn_sched_barrier(0);
       comp(t, B);
-      if (ta >= ntiles) break;
+      if (ta >= tend) break;
       t = ta;
     }
     return;
@@ -287,8 +296,8 @@ int main(int argc, char **argv) {
   };
 
   if (getenv("TUNE_FEW"))
-    vs = {V(10, 16, 1024, 1, true, true, 0, 1), V(10, 16, 1024, 1, true, true, 1, 1), V(10, 16, 1024, 1, true, true, 2, 1),
-          V(10, 16, 1024, 1, true, true, 3, 1), V(10, 8, 1024, 1, true, true, 3, 1), V(10, 8, 512, 1, true, true, 3, 2)};
+    vs = {V(10, 16, 1024, 1, true, true, 3, 1), V(10, 16, 1024, 1, true, true, 4, 1), V(10, 8, 512, 1, true, true, 4, 2),
+          V(10, 16, 1024, 1, true, true, 3, 1), V(10, 16, 1024, 1, true, true, 4, 1)};
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
