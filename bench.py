@@ -156,34 +156,18 @@ def wl_repair12(args, ctx, stream, rank):
     """Config 4: RS(12,4) single-failure repair; fused (k+1) recover and the
     unfused agent partial-encode path (racks of 4 chunks: partial 1 x g encodes,
     container_manager.cc:251, then the CAR XOR finalize, rs.cc:94-109)."""
-    import numpy as np
-
     n, k, cs, ns, g = 16, 12, args.chunk, args.stripes, 4
     stripe = n * cs
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xBEEF + rank)
     ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream)
     failed = args.failed if args.failed is not None else 0
-    ids, _, rm = nxec.rs_plan(n, k, [failed], True)
-    ids = ids[:k]
-    groups = []  # (start index in ids, size) per rack
-    j = 0
-    while j < k:
-        rack, st = ids[j] // g, j
-        while j < k and ids[j] // g == rack:
-            j += 1
-        groups.append((st, j - st))
-    G = len(groups)
+    racks = [list(range(r, min(r + g, n))) for r in range(0, n, g)]  # chunk i on agent i // g
+    G = len(nxec.car_plan(n, k, failed, racks))
     part = nxec.DeviceBuffer(ns * G * cs)
-    ones = np.ones((1, G), dtype=np.uint8)
 
     def unfused(i):
-        for gi, (st, sz) in enumerate(groups):
-            ctx.stripes_mul(rm[:, st:st + sz], buf.ptr, part.ptr, src_idx=ids[st:st + sz], dst_idx=[gi],
-                            src_chunk_stride=cs, src_stripe_stride=stripe, dst_chunk_stride=cs,
-                            dst_stripe_stride=G * cs, length=cs, nstripes=ns, stream=stream)
-        ctx.stripes_mul(ones, part.ptr, buf.ptr, dst_idx=[failed], src_chunk_stride=cs, src_stripe_stride=G * cs,
-                        dst_chunk_stride=cs, dst_stripe_stride=stripe, length=cs, nstripes=ns, stream=stream)
+        ctx.rs_car_repair(n, k, failed, racks, buf.ptr, cs, stripe, part.ptr, G * cs, cs, ns, stream)
 
     ops = [
         ("repair_fused", lambda i: ctx.rs_recover(n, k, [failed], buf.ptr, cs, stripe, cs, ns, stream),

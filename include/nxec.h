@@ -161,6 +161,28 @@ int nxec_rs_plan(int n, int k, const int32_t *failed, int nfailed, int is_repair
 int nxec_rs_decode_matrix(int n, int k, const int32_t *input_ids, const int32_t *targets, int ntargets,
                           unsigned char *out);
 
+/* Cross-rack-aware (CAR) single-failure repair plan, chunk_manager.cc:929-986:
+ * given the racks' chunk-id lists (as the coordinator's findChunkGroups
+ * reports them: group g holds group_chunks[group_offsets[g] .. group_offsets[g+1])),
+ * keep in each rack only the chunks chosen as repair inputs (the first k alive,
+ * rs.cc:252-265) and attach to each its coefficient of the repair row.  Output:
+ * *nsub sub-groups (sub_offsets[0..*nsub], sub_chunks, sub_coeffs in group
+ * order; racks with no selected chunk are skipped).  Each sub-group is one
+ * agent's partial encode (ENC_CHUNK_REQ, container_manager.cc:221-258); the
+ * XOR of the partials is the lost chunk (rs.cc:94-109). */
+int nxec_car_plan(int n, int k, int failed, const int32_t *group_offsets, const int32_t *group_chunks, int ngroups,
+                  int32_t *sub_offsets, int32_t *sub_chunks, unsigned char *sub_coeffs, int *nsub);
+
+/* Device-resident CAR repair over a batch: per stripe, one partial encode per
+ * sub-group of the plan above into d_partials ([s][nsub][len], caller scratch,
+ * partial_stripe_stride bytes per stripe), then the all-ones XOR of the
+ * partials into chunk `failed` of d_stripes -- the agents' and proxy's work of
+ * a CAR repair (agent.cc:240-415) on one GPU. */
+int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const int32_t *group_offsets,
+                               const int32_t *group_chunks, int ngroups, unsigned char *d_stripes, int64_t chunk_stride,
+                               int64_t stripe_stride, unsigned char *d_partials, int64_t partial_stripe_stride,
+                               int64_t len, int64_t nstripes, void *stream);
+
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU
  *    framework can drive section 3.  Thin wrappers over the HIP runtime.

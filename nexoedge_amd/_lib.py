@@ -51,6 +51,11 @@ _PROTOS = {
         C.c_int,
         [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, i64, vp],
     ),
+    "nxec_car_plan": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp, C.POINTER(C.c_int)]),
+    "nxec_rs_car_repair_stripes": (
+        C.c_int,
+        [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, vp],
+    ),
     "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
     "nxec_rs_plan": (C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
     "nxec_rs_decode_matrix": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp]),

@@ -192,3 +192,40 @@ extern "C" int nxec_rs_decode_matrix(int n, int k, const int32_t *input_ids, con
   if (rc != NXEC_OK) return set_error(rc, "nxec_rs_decode_matrix: inputs do not form an invertible matrix");
   return NXEC_OK;
 }
+
+extern "C" int nxec_car_plan(int n, int k, int failed, const int32_t *group_offsets, const int32_t *group_chunks,
+                             int ngroups, int32_t *sub_offsets, int32_t *sub_chunks, unsigned char *sub_coeffs,
+                             int *nsub) {
+  using namespace nxec;
+  if (nsub) *nsub = 0;
+  if (!valid_nk(n, k) || n == k || failed < 0 || failed >= n || ngroups < 0 || (ngroups > 0 && (!group_offsets || !group_chunks)) ||
+      !sub_offsets || !sub_chunks || !sub_coeffs || !nsub)
+    return set_error(NXEC_ERR_INVALID, "nxec_car_plan: invalid arguments");
+  std::vector<int32_t> inputs(n);
+  std::vector<uint8_t> row(k);
+  int ni = 0, mi = 0;
+  const int32_t f = failed;
+  int rc = nxec_rs_plan(n, k, &f, 1, 1, inputs.data(), &ni, &mi, row.data());
+  if (rc) return rc;
+  // chunk id -> position among the k selected inputs (chunk_manager.cc:932-936)
+  std::vector<int> pos(n, -1);
+  for (int i = 0; i < k; i++) pos[inputs[i]] = i;
+  int filled = 0, ns = 0;
+  sub_offsets[0] = 0;
+  for (int g = 0; g < ngroups && filled < k; g++) {  // scan racks until every input is placed (:939)
+    const int before = filled;
+    for (int c = group_offsets[g]; c < group_offsets[g + 1]; c++) {
+      const int cid = group_chunks[c];
+      if (cid < 0 || cid >= n) return set_error(NXEC_ERR_INVALID, "nxec_car_plan: chunk id %d out of range", cid);
+      if (pos[cid] < 0) continue;
+      sub_chunks[filled] = cid;
+      sub_coeffs[filled] = row[pos[cid]];
+      pos[cid] = -1;  // a chunk listed twice is used once
+      filled++;
+    }
+    if (filled > before) sub_offsets[++ns] = filled;
+  }
+  if (filled != k) return set_error(NXEC_ERR_INVALID, "nxec_car_plan: racks cover %d of the %d repair inputs", filled, k);
+  *nsub = ns;
+  return NXEC_OK;
+}

@@ -79,6 +79,29 @@ def decode_matrix(n: int, k: int, input_ids: Sequence[int], targets: Sequence[in
     return out[: len(targets)]
 
 
+def _groups(groups: Sequence[Sequence[int]]):
+    offs = [0]
+    flat = []
+    for g in groups:
+        flat.extend(int(c) for c in g)
+        offs.append(len(flat))
+    o, op = _i32(offs)
+    c, cp = _i32(flat if flat else [0])
+    return (o, c), op, cp
+
+
+def car_plan(n: int, k: int, failed: int, groups: Sequence[Sequence[int]]):
+    """CAR repair plan (chunk_manager.cc:929-986) -> list of (chunk_ids, coeffs) per agent sub-group."""
+    keep, op, cp = _groups(groups)
+    so = np.zeros(len(groups) + 2, dtype=np.int32)
+    sc = np.zeros(k, dtype=np.int32)
+    cf = np.zeros(k, dtype=np.uint8)
+    ns = C.c_int(0)
+    check(lib.nxec_car_plan(n, k, failed, op, cp, len(groups), C.c_void_p(so.ctypes.data), C.c_void_p(sc.ctypes.data),
+                            _u8(cf), C.byref(ns)), "nxec_car_plan")
+    return [(sc[so[g]:so[g + 1]].tolist(), cf[so[g]:so[g + 1]].copy()) for g in range(ns.value)]
+
+
 # ------------------------------------------------------- host-buffer encode
 def encode_host(coeffs: np.ndarray, data: Sequence[np.ndarray]) -> list:
     """CodingUtils::encode / ec_encode_data on host buffers (GPU-executed)."""
@@ -269,6 +292,14 @@ class Context:
                                          chunk_stride, stripe_stride, C.c_void_p(int(out)), out_chunk_stride,
                                          out_stripe_stride, length, nstripes, stream), "nxec_rs_decode_stripes")
 
+    def rs_car_repair(self, n: int, k: int, failed: int, groups, stripes: int, chunk_stride: int, stripe_stride: int,
+                      partials: int, partial_stripe_stride: int, length: int, nstripes: int, stream=None) -> None:
+        keep, op, cp = _groups(groups)
+        check(lib.nxec_rs_car_repair_stripes(C.c_void_p(self.ptr), n, k, failed, op, cp, len(groups),
+                                             C.c_void_p(int(stripes)), chunk_stride, stripe_stride,
+                                             C.c_void_p(int(partials)), partial_stripe_stride, length, nstripes, stream),
+              "nxec_rs_car_repair_stripes")
+
     def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
                              batch_stripes: int = 0) -> None:
         check(lib.nxec_rs_encode_host_batch(C.c_void_p(self.ptr), n, k, C.c_void_p(int(h_data)),
@@ -288,6 +319,6 @@ class Context:
 
 __all__ = [
     "NxecError", "gf_mul", "gf_inv", "gen_rs_matrix", "invert_matrix", "init_tables", "rs_plan", "decode_matrix",
-    "encode_host", "ec_encode_data", "device_count", "device_info", "device_sync", "DeviceBuffer", "PinnedBuffer",
+    "encode_host", "ec_encode_data", "car_plan", "device_count", "device_info", "device_sync", "DeviceBuffer", "PinnedBuffer",
     "Event", "Context",
 ]

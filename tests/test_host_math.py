@@ -71,3 +71,33 @@ def test_decode_matrix_rows_are_consistent():
                 s ^= nxec.gf_mul(int(inv[l, j]), int(enc[t, l]))
             want[j] = s
         assert np.array_equal(m[row], want)
+
+
+def test_car_plan_matches_reference_grouping(golden):
+    """CAR planning (chunk_manager.cc:929-986) against the golden CAR cases:
+    racks of g chunks (chunk i on rack i // g)."""
+    for c in golden["car"]:
+        n, k, f, g = c["n"], c["k"], c["failed"], c["rack_size"]
+        racks = [list(range(r, min(r + g, n))) for r in range(0, n, g)]
+        subs = nxec.car_plan(n, k, f, racks)
+        row = bytes.fromhex(c["repair_row_hex"])
+        ids, _, _ = nxec.rs_plan(n, k, [f], True)
+        assert [len(ch) for ch, _ in subs] == [size for _, size in c["groups"]]
+        for (chunks, coeffs), (start, size) in zip(subs, c["groups"]):
+            assert chunks == ids[start:start + size]
+            assert bytes(coeffs) == row[start:start + size]
+
+
+def test_car_plan_unordered_racks_and_errors():
+    import pytest
+    n, k = 16, 12
+    racks = [[12, 13, 14, 15], [3, 1, 0, 2], [7, 6, 5, 4], [8, 9, 10, 11]]
+    subs = nxec.car_plan(n, k, 5, racks)
+    ids, _, rm = nxec.rs_plan(n, k, [5], True)
+    pos = {cid: i for i, cid in enumerate(ids[:k])}
+    flat = [(cid, int(cf)) for ch, cfs in subs for cid, cf in zip(ch, cfs)]
+    assert sorted(c for c, _ in flat) == sorted(ids[:k])
+    assert all(cf == rm[0][pos[cid]] for cid, cf in flat)
+    assert [ch for ch, _ in subs][:2] == [[12], [3, 1, 0, 2]]  # rack order and in-rack order kept
+    with pytest.raises(nxec.NxecError):
+        nxec.car_plan(n, k, 5, [[0, 1, 2]])  # racks do not cover the inputs
