@@ -183,6 +183,14 @@ int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const 
                                int64_t stripe_stride, unsigned char *d_partials, int64_t partial_stripe_stride,
                                int64_t len, int64_t nstripes, void *stream);
 
+/* MD5 digest of every chunk of a device-resident batch: the
+ * checksum the reference computes per chunk on writes and repairs
+ * (chunk_manager.cc:175,1173, agent.cc:342 -> Chunk::computeMD5, chunk.hh:136).
+ * Chunk c of stripe s at d_base + s*stripe_stride + c*chunk_stride, len bytes;
+ * digest (16 bytes, RFC 1321 byte order) at d_digests[(s*nchunks + c)*16]. */
+int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
+                    int nchunks, int64_t len, int64_t nstripes, unsigned char *d_digests, void *stream);
+
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU
  *    framework can drive section 3.  Thin wrappers over the HIP runtime.

@@ -62,6 +62,8 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).
 int prepare_kernels();
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream);
+int launch_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride, int nchunks, int64_t len,
+               int64_t nstripes, uint8_t *digests, void *stream);
 int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
 
 }  // namespace nxec

@@ -399,6 +399,15 @@ int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const 
                           chunk_stride, stripe_stride, nullptr, len, nstripes, stream);
 }
 
+int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
+                    int nchunks, int64_t len, int64_t nstripes, unsigned char *d_digests, void *stream) {
+  if (!ctx || nchunks < 0 || len < 0 || nstripes < 0 || ((nchunks > 0 && nstripes > 0) && (!d_base || !d_digests)))
+    return set_error(NXEC_ERR_INVALID, "nxec_md5_chunks: invalid arguments");
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  return launch_md5(d_base, chunk_stride, stripe_stride, nchunks, len, nstripes, d_digests, pick_stream(ctx, stream));
+}
+
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,
                               int64_t len, int64_t nstripes, int64_t batch_stripes) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");

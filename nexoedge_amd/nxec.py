@@ -300,6 +300,11 @@ class Context:
                                              C.c_void_p(int(partials)), partial_stripe_stride, length, nstripes, stream),
               "nxec_rs_car_repair_stripes")
 
+    def md5_chunks(self, base: int, chunk_stride: int, stripe_stride: int, nchunks: int, length: int, nstripes: int,
+                   digests: int, stream=None) -> None:
+        check(lib.nxec_md5_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride, nchunks,
+                                  length, nstripes, C.c_void_p(int(digests)), stream), "nxec_md5_chunks")
+
     def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
                              batch_stripes: int = 0) -> None:
         check(lib.nxec_rs_encode_host_batch(C.c_void_p(self.ptr), n, k, C.c_void_p(int(h_data)),
