@@ -35,8 +35,8 @@ $(LIBDIR)/libnxec.so: $(LIB_OBJS)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(LIB_OBJS) -o $@
 
-oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_oracle.h
-	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c -o $@ -lpthread
+oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_oracle.h
+	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c oracle/nxec_cpu_simd.c -o $@ -lpthread
 
 # design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
 tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling

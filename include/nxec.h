@@ -177,11 +177,12 @@ int nxec_car_plan(int n, int k, int failed, const int32_t *group_offsets, const 
  * sub-group of the plan above into d_partials ([s][nsub][len], caller scratch,
  * partial_stripe_stride bytes per stripe), then the all-ones XOR of the
  * partials into chunk `failed` of d_stripes -- the agents' and proxy's work of
- * a CAR repair (agent.cc:240-415) on one GPU. */
+ * a CAR repair (agent.cc:240-415) on one GPU.  Partial g of stripe s is at
+ * d_partials + s * partial_stripe_stride + g * partial_chunk_stride. */
 int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const int32_t *group_offsets,
                                const int32_t *group_chunks, int ngroups, unsigned char *d_stripes, int64_t chunk_stride,
-                               int64_t stripe_stride, unsigned char *d_partials, int64_t partial_stripe_stride,
-                               int64_t len, int64_t nstripes, void *stream);
+                               int64_t stripe_stride, unsigned char *d_partials, int64_t partial_chunk_stride,
+                               int64_t partial_stripe_stride, int64_t len, int64_t nstripes, void *stream);
 
 /* MD5 digest of every chunk of a device-resident batch: the
  * checksum the reference computes per chunk on writes and repairs

@@ -54,7 +54,7 @@ _PROTOS = {
     "nxec_car_plan": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, vp, vp, C.POINTER(C.c_int)]),
     "nxec_rs_car_repair_stripes": (
         C.c_int,
-        [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, vp],
+        [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, i64, vp],
     ),
     "nxec_md5_chunks": (C.c_int, [vp, vp, i64, i64, C.c_int, i64, i64, vp, vp]),
     "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),

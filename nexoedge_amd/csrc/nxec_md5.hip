@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "nxec_internal.h"
 
@@ -81,10 +82,12 @@ __device__ __forceinline__ void md5_block(uint32_t (&h)[4], const uint32_t (&m)[
   md5_rounds(h, m, std::make_integer_sequence<int, 64>{});
 }
 
+template <bool NT>
 __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t (&m)[16]) {
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p) + i);
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p) + i;
+    const u32x4 v = NT ? __builtin_nontemporal_load(q) : *q;
     m[4 * i] = v.x;
     m[4 * i + 1] = v.y;
     m[4 * i + 2] = v.z;
@@ -92,7 +95,37 @@ __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t (&m)[16]) 
   }
 }
 
+// Aligned streaming of the full 64-byte blocks with a ring of D block buffers:
+// block b+D-1 is loaded while block b is hashed, so D-1 blocks (~0.75 us of
+// rounds each) cover the HBM latency.  The ring is fully unrolled so every
+// buffer is a fixed register set and the load->use distance is explicit to
+// the waitcnt pass (a loop-carried copy of a prefetch buffer makes it wait on
+// the loads it just issued).  Loads past the last block are clamped to it
+// (re-reading one block) so they can stay unconditional.
+template <int D, bool NT>
+__device__ __forceinline__ void md5_stream(const uint8_t *p, int64_t nfull, uint32_t (&h)[4]) {
+  uint32_t ring[D][16];
+  const int64_t last = nfull - 1;
+#pragma unroll
+  for (int j = 0; j < D - 1; j++) load_block<NT>(p + min(static_cast<int64_t>(j), last) * 64, ring[j]);
+  int64_t b = 0;
+  for (; b + D <= nfull; b += D) {
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+      load_block<NT>(p + min(b + j + D - 1, last) * 64, ring[(j + D - 1) % D]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this block's rounds
+      md5_block(h, ring[j]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // the last nfull % D (< D) blocks are already in ring[0 .. D-2]
+#pragma unroll
+  for (int j = 0; j < D - 1; j++)
+    if (b + j < nfull) md5_block(h, ring[j]);
+}
+
 // one lane per chunk; chunk c of the batch = stripe c / nchunks, index c % nchunks
+template <int D, bool NT>
 __global__ __launch_bounds__(64) void k_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride,
                                             int nchunks, int64_t len, int64_t total, uint8_t *digests,
                                             int aligned) {
@@ -104,16 +137,7 @@ __global__ __launch_bounds__(64) void k_md5(const uint8_t *base, int64_t chunk_s
   const int64_t nfull = len / 64;
   uint32_t m[16];
   if (aligned) {
-    if (nfull > 0) {
-      uint32_t nx[16];
-      load_block(p, m);
-      for (int64_t b = 0; b < nfull; b++) {
-        if (b + 1 < nfull) load_block(p + (b + 1) * 64, nx);  // next block in flight during the rounds
-        md5_block(h, m);
-#pragma unroll
-        for (int i = 0; i < 16; i++) m[i] = nx[i];
-      }
-    }
+    if (nfull > 0) md5_stream<D, NT>(p, nfull, h);
   } else {
     for (int64_t b = 0; b < nfull; b++) {
 #pragma unroll
@@ -155,6 +179,23 @@ __global__ __launch_bounds__(64) void k_md5(const uint8_t *base, int64_t chunk_s
   o[3] = h[3];
 }
 
+int md5_depth() {
+  static const int d = [] {
+    const char *e = getenv("NXEC_MD5_DEPTH");  // tuning override: prefetch ring depth 2..4
+    const int v = e ? atoi(e) : 3;
+    return v >= 2 && v <= 4 ? v : 3;
+  }();
+  return d;
+}
+
+bool md5_nontemporal() {
+  static const bool nt = [] {
+    const char *e = getenv("NXEC_MD5_NT");  // tuning override: 0 = cached loads
+    return !(e && e[0] == '0');
+  }();
+  return nt;
+}
+
 }  // namespace
 
 int launch_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride, int nchunks, int64_t len,
@@ -164,7 +205,11 @@ int launch_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride,
   const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (chunk_stride % 16 == 0) &&
                        (stripe_stride % 16 == 0);
   const int64_t blocks = (total + 63) / 64;
-  hipLaunchKernelGGL(k_md5, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream), base,
+  const int d = md5_depth();
+  const bool nt = md5_nontemporal();
+  auto kern = nt ? (d == 2 ? k_md5<2, true> : d == 4 ? k_md5<4, true> : k_md5<3, true>)
+                 : (d == 2 ? k_md5<2, false> : d == 4 ? k_md5<4, false> : k_md5<3, false>);
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream), base,
                      chunk_stride, stripe_stride, nchunks, len, total, digests, aligned ? 1 : 0);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_md5: %s", hipGetErrorString(e));

@@ -378,24 +378,26 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
 
 int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const int32_t *group_offsets,
                                const int32_t *group_chunks, int ngroups, unsigned char *d_stripes, int64_t chunk_stride,
-                               int64_t stripe_stride, unsigned char *d_partials, int64_t partial_stripe_stride,
-                               int64_t len, int64_t nstripes, void *stream) {
+                               int64_t stripe_stride, unsigned char *d_partials, int64_t partial_chunk_stride,
+                               int64_t partial_stripe_stride, int64_t len, int64_t nstripes, void *stream) {
   if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
   std::vector<int32_t> so(static_cast<size_t>(std::max(ngroups, 0)) + 2), sc(k);
   std::vector<unsigned char> cf(k);
   int ns = 0;
   int rc = nxec_car_plan(n, k, failed, group_offsets, group_chunks, ngroups, so.data(), sc.data(), cf.data(), &ns);
   if (rc) return rc;
-  if (!d_partials || partial_stripe_stride < ns * len) return set_error(NXEC_ERR_INVALID, "partials buffer too small");
+  if (!d_partials || partial_chunk_stride < len || partial_stripe_stride < (ns - 1) * partial_chunk_stride + len)
+    return set_error(NXEC_ERR_INVALID, "nxec_rs_car_repair_stripes: partials layout too small");
   for (int g = 0; g < ns; g++) {  // agent partial encodes (container_manager.cc:251)
     const int32_t dst = g;
     rc = nxec_stripes_mul(ctx, 1, so[g + 1] - so[g], cf.data() + so[g], d_stripes, sc.data() + so[g], chunk_stride,
-                          stripe_stride, d_partials, &dst, len, partial_stripe_stride, nullptr, len, nstripes, stream);
+                          stripe_stride, d_partials, &dst, partial_chunk_stride, partial_stripe_stride, nullptr, len,
+                          nstripes, stream);
     if (rc) return rc;
   }
   std::vector<unsigned char> ones(ns, 1);  // CAR finalize: XOR of the partials (rs.cc:94-109)
   const int32_t tgt = failed;
-  return nxec_stripes_mul(ctx, 1, ns, ones.data(), d_partials, nullptr, len, partial_stripe_stride, d_stripes, &tgt,
+  return nxec_stripes_mul(ctx, 1, ns, ones.data(), d_partials, nullptr, partial_chunk_stride, partial_stripe_stride, d_stripes, &tgt,
                           chunk_stride, stripe_stride, nullptr, len, nstripes, stream);
 }
 

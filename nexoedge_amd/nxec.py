@@ -293,11 +293,13 @@ class Context:
                                          out_stripe_stride, length, nstripes, stream), "nxec_rs_decode_stripes")
 
     def rs_car_repair(self, n: int, k: int, failed: int, groups, stripes: int, chunk_stride: int, stripe_stride: int,
-                      partials: int, partial_stripe_stride: int, length: int, nstripes: int, stream=None) -> None:
+                      partials: int, partial_chunk_stride: int, partial_stripe_stride: int, length: int, nstripes: int,
+                      stream=None) -> None:
         keep, op, cp = _groups(groups)
         check(lib.nxec_rs_car_repair_stripes(C.c_void_p(self.ptr), n, k, failed, op, cp, len(groups),
                                              C.c_void_p(int(stripes)), chunk_stride, stripe_stride,
-                                             C.c_void_p(int(partials)), partial_stripe_stride, length, nstripes, stream),
+                                             C.c_void_p(int(partials)), partial_chunk_stride, partial_stripe_stride, length,
+                                             nstripes, stream),
               "nxec_rs_car_repair_stripes")
 
     def md5_chunks(self, base: int, chunk_stride: int, stripe_stride: int, nchunks: int, length: int, nstripes: int,

@@ -98,6 +98,25 @@ def matmul(coeffs: np.ndarray, srcs: Sequence[np.ndarray]) -> List[np.ndarray]:
     return outs
 
 
+_o.orc_simd_level.restype = C.c_int
+_o.orc_simd_encode.restype = C.c_int
+_o.orc_simd_encode.argtypes = [C.c_int, C.c_size_t, C.c_int, C.c_int, vp, vp, vp]
+
+
+def simd_level() -> int:
+    """512 (AVX-512BW), 256 (AVX2) or 0: the CPU-baseline SIMD path this host runs."""
+    return _o.orc_simd_level()
+
+
+def simd_encode(coeffs: np.ndarray, srcs: Sequence[np.ndarray], outs: Sequence[np.ndarray], level: int = -1) -> int:
+    """CPU baseline stand-in for ISA-L's SIMD ec_encode_data (nxec_cpu_simd.c):
+    outs[r] = sum_j coeffs[r, j] * srcs[j].  Writes into `outs`; returns the level used."""
+    c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    rows, k = c.shape
+    return _o.orc_simd_encode(level, len(srcs[0]), k, rows, _p(c), (vp * k)(*[s.ctypes.data for s in srcs]),
+                              (vp * rows)(*[o.ctypes.data for o in outs]))
+
+
 def encode_data(gftbls: np.ndarray, k: int, rows: int, srcs: Sequence[np.ndarray]) -> List[np.ndarray]:
     n = len(srcs[0])
     t = np.ascontiguousarray(gftbls, dtype=np.uint8)

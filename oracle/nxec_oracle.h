@@ -71,6 +71,13 @@ void orc_fill_bytes(uint8_t *p, int64_t nbytes, uint64_t seed);
 double orc_time_encode(int k, int rows, const uint8_t *a, const uint8_t *src, uint8_t *dst,
                        int64_t cs, int64_t nstripes, int threads);
 
+/* CPU baseline stand-in for ISA-L's SIMD kernels (nxec_cpu_simd.c):
+ * split-nibble vpshufb, AVX-512BW (level 512) / AVX2 (256) / scalar (0);
+ * level -1 = best available.  Returns the level used. */
+int orc_simd_level(void);
+int orc_simd_encode(int level, size_t len, int k, int rows, const uint8_t *coef, const uint8_t *const *src,
+                    uint8_t *const *dst);
+
 #ifdef __cplusplus
 }
 #endif

@@ -355,7 +355,7 @@ def test_car_repair_stripes_golden(gpu_ctx, golden):
         hb[:, :, :cs] = host
         sb = up(hb)
         pb = nxec.DeviceBuffer(ns * len(c["groups"]) * stride)
-        gpu_ctx.rs_car_repair(n, k, f, racks, sb.ptr, stride, n * stride, pb.ptr, len(c["groups"]) * stride, cs, ns)
+        gpu_ctx.rs_car_repair(n, k, f, racks, sb.ptr, stride, n * stride, pb.ptr, stride, len(c["groups"]) * stride, cs, ns)
         gpu_ctx.sync()
         out = sb.download().reshape(ns, n, stride)[:, :, :cs]
         parts = pb.download().reshape(ns, len(c["groups"]), stride)[:, :, :cs]

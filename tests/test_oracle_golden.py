@@ -136,3 +136,20 @@ def test_oracle_matches_reference_library_random():
         ref.encode(coeffs, srcs, want)
         got = oracle.matmul(coeffs, srcs)
         assert all(np.array_equal(g, w) for g, w in zip(got, want))
+
+
+@pytest.mark.parametrize("level", [0, 256, 512])
+def test_cpu_simd_baseline_matches_oracle(level):
+    """The CPU-baseline SIMD stand-in (oracle/nxec_cpu_simd.c) is bit-exact with the
+    oracle for ragged lengths and 1..9 rows (multi-pass)."""
+    if level > oracle.simd_level():
+        pytest.skip(f"host lacks SIMD level {level}")
+    rng = np.random.default_rng(level + 3)
+    for k, rows, length in [(10, 4, 4096 + 77), (1, 1, 63), (12, 1, 200), (16, 9, 1000), (4, 3, 64 * 5 + 31), (7, 2, 5)]:
+        c = rng.integers(0, 256, size=(rows, k), dtype=np.uint8)
+        srcs = [rng.integers(0, 256, size=length, dtype=np.uint8) for _ in range(k)]
+        outs = [np.zeros(length, dtype=np.uint8) for _ in range(rows)]
+        assert oracle.simd_encode(c, srcs, outs, level) == level
+        want = oracle.matmul(c, srcs)
+        for r in range(rows):
+            assert np.array_equal(outs[r], want[r]), (k, rows, length, r)
