@@ -192,6 +192,40 @@ int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const 
 int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
                     int nchunks, int64_t len, int64_t nstripes, unsigned char *d_digests, void *stream);
 
+/* ---- Object-level batched entry (ChunkManager write/read of a
+ * whole object in one call instead of the per-stripe loop of
+ * proxy_file_ops.cc:557-666 / chunk_manager.cc:99,787).
+ *
+ * Layout of an object of `length` bytes under (n,k) and max chunk size M
+ * (storage class max_chunk_size): full stripes hold k*M data bytes with
+ * chunk size M; a remainder r > 0 forms one last stripe with chunk size
+ * ceil(r/k) (RSCode::getChunkSize, rs.cc:52-55), zero-padded to k chunks
+ * (chunk_manager.cc:390-399).  Chunk (s, i) has id s*n + i
+ * (chunk_manager.cc:441-447). */
+int nxec_object_layout(int n, int k, int64_t length, int64_t max_chunk_size, int64_t *nstripes,
+                       int64_t *full_stripes, int64_t *last_chunk_size);
+
+/* Encode an object resident in HBM.  Data chunks are read in place (full
+ * stripes: chunk (s, j) = d_object + s*k*M + j*M).  Parity chunk (s, i) is
+ * written at d_parity + (s*(n-k) + i)*M ([nstripes][n-k][M]; the last stripe
+ * uses the first last_chunk_size bytes of its slots).  d_tail (k*M bytes, may
+ * be NULL when length is a multiple of k*M) receives the zero-padded data
+ * chunks of the last stripe at j*last_chunk_size.  d_md5 (NULL = skip):
+ * [nstripes][n][16] MD5 digests of every chunk (Chunk::computeMD5 of
+ * writeFileStripe, chunk_manager.cc:175), one kernel launch. */
+int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_object, int64_t length,
+                       int64_t max_chunk_size, unsigned char *d_parity, unsigned char *d_tail, unsigned char *d_md5,
+                       void *stream);
+
+/* Read path (decodeFile, chunk_manager.cc:738-800, batched): chunks of the
+ * object as fetched, chunk (s, i) at d_chunks + (s*n + i)*M (last stripe:
+ * last_chunk_size bytes per slot), chunks `failed` (ascending, same for every
+ * stripe) absent.  Writes the `length` object bytes to d_object; d_tail is
+ * k*M bytes of scratch (may be NULL when length is a multiple of k*M). */
+int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                       const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
+                       unsigned char *d_tail, void *stream);
+
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU
  *    framework can drive section 3.  Thin wrappers over the HIP runtime.

@@ -62,8 +62,20 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).
 int prepare_kernels();
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream);
-int launch_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride, int nchunks, int64_t len,
-               int64_t nstripes, uint8_t *digests, void *stream);
+// One MD5 launch hashes up to kMaxMd5Regions chunk sets: region r covers
+// chunks (s, i), s < nstripes, i < nchunks, at base + s*stripe_stride +
+// i*chunk_stride, each `len` bytes; digest at digests + s*dig_stripe_stride +
+// i*16.  (A chain per chunk: one launch for everything, so its time is one
+// chunk's hash, not a sum.)
+constexpr int kMaxMd5Regions = 4;
+struct Md5Region {
+  const uint8_t *base;
+  int64_t chunk_stride, stripe_stride, len, nstripes;
+  uint8_t *digests;
+  int64_t dig_stripe_stride;
+  int nchunks;
+};
+int launch_md5(const Md5Region *regions, int nregions, void *stream);
 int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
 
 }  // namespace nxec

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "nxec_internal.h"
@@ -45,23 +46,15 @@ template <int R>
 __device__ __forceinline__ void md5_round(uint32_t &a, uint32_t b, uint32_t c, uint32_t d, const uint32_t (&m)[16]) {
   constexpr int kShift[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
   constexpr int q = R / 16;
-  uint32_t f;
-  int g;
-  if (q == 0) {
-    f = (b & c) | (~b & d);  // v_bfi
-    g = R;
-  } else if (q == 1) {
-    f = (d & b) | (~d & c);
-    g = (5 * R + 1) & 15;
-  } else if (q == 2) {
-    f = b ^ c ^ d;
-    g = (3 * R + 5) & 15;
-  } else {
-    f = c ^ (b | ~d);
-    g = (7 * R) & 15;
-  }
-  constexpr uint32_t kr = kMd5K[R];  // compile-time constant: an instruction literal, no load
-  a = b + rotl(a + f + kr + m[g], kShift[q][R & 3]);
+  // one v_bitop3_b32 per round function (truth table over (b, c, d), bit
+  // index 4b+2c+d): F = b ? c : d (0xCA), G = d ? b : c (0xE4),
+  // H = b ^ c ^ d (0x96), I = c ^ (b | ~d) (0x39)
+  constexpr unsigned kTruth[4] = {0xCA, 0xE4, 0x96, 0x39};
+  const uint32_t f = __builtin_amdgcn_bitop3_b32(b, c, d, kTruth[q]);
+  constexpr int g = q == 0 ? R : q == 1 ? (5 * R + 1) & 15 : q == 2 ? (3 * R + 5) & 15 : (7 * R) & 15;
+  constexpr uint32_t kr = kMd5K[R];  // compile-time constant: no load
+  const uint32_t x = a + kr + m[g];    // off the critical path: a is 4 rounds old
+  a = b + rotl(f + x, kShift[q][R & 3]);
 }
 
 template <int... Rs>
@@ -95,49 +88,83 @@ __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t (&m)[16]) 
   }
 }
 
-// Aligned streaming of the full 64-byte blocks with a ring of D block buffers:
-// block b+D-1 is loaded while block b is hashed, so D-1 blocks (~0.75 us of
-// rounds each) cover the HBM latency.  The ring is fully unrolled so every
-// buffer is a fixed register set and the load->use distance is explicit to
-// the waitcnt pass (a loop-carried copy of a prefetch buffer makes it wait on
-// the loads it just issued).  Loads past the last block are clamped to it
-// (re-reading one block) so they can stay unconditional.
-template <int D, bool NT>
-__device__ __forceinline__ void md5_stream(const uint8_t *p, int64_t nfull, uint32_t (&h)[4]) {
-  uint32_t ring[D][16];
-  const int64_t last = nfull - 1;
+// Aligned streaming of the full 64-byte blocks.  A lane reads its chunk in
+// groups of G blocks (G*64 contiguous bytes issued back to back, so the
+// memory system sees G*64-byte runs per chunk instead of scattered 64-byte
+// pieces from ~57k concurrent streams) through a ring of D group buffers:
+// group g+D-1 is loaded while group g is hashed.  The ring is fully unrolled
+// so every buffer is a fixed register set and the load->use distance is
+// explicit to the waitcnt pass (a loop-carried copy of a prefetch buffer makes
+// it wait on the loads it just issued).  Loads past the last group are
+// clamped to it (re-reading it) so they stay unconditional; the < G leftover
+// blocks are read one at a time.
+template <int G, bool NT>
+__device__ __forceinline__ void load_group(const uint8_t *p, uint32_t (&m)[G][16]) {
 #pragma unroll
-  for (int j = 0; j < D - 1; j++) load_block<NT>(p + min(static_cast<int64_t>(j), last) * 64, ring[j]);
-  int64_t b = 0;
-  for (; b + D <= nfull; b += D) {
-#pragma unroll
-    for (int j = 0; j < D; j++) {
-      load_block<NT>(p + min(b + j + D - 1, last) * 64, ring[(j + D - 1) % D]);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this block's rounds
-      md5_block(h, ring[j]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  // the last nfull % D (< D) blocks are already in ring[0 .. D-2]
-#pragma unroll
-  for (int j = 0; j < D - 1; j++)
-    if (b + j < nfull) md5_block(h, ring[j]);
+  for (int i = 0; i < G; i++) load_block<NT>(p + 64 * i, m[i]);
 }
 
-// one lane per chunk; chunk c of the batch = stripe c / nchunks, index c % nchunks
-template <int D, bool NT>
-__global__ __launch_bounds__(64) void k_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride,
-                                            int nchunks, int64_t len, int64_t total, uint8_t *digests,
-                                            int aligned) {
+template <int D, int G, bool NT>
+__device__ __forceinline__ void md5_stream(const uint8_t *p, int64_t nfull, uint32_t (&h)[4]) {
+  constexpr int64_t kGroup = 64 * G;
+  const int64_t ngroups = nfull / G;
+  if (ngroups > 0) {
+    uint32_t ring[D][G][16];
+    const int64_t last = ngroups - 1;
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load_group<G, NT>(p + min(static_cast<int64_t>(j), last) * kGroup, ring[j]);
+    int64_t g = 0;
+    for (; g + D <= ngroups; g += D) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        load_group<G, NT>(p + min(g + j + D - 1, last) * kGroup, ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this group's rounds
+#pragma unroll
+        for (int i = 0; i < G; i++) md5_block(h, ring[j][i]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // the last ngroups % D (< D) groups are already in ring[0 .. D-2]
+#pragma unroll
+    for (int j = 0; j < D - 1; j++)
+      if (g + j < ngroups) {
+#pragma unroll
+        for (int i = 0; i < G; i++) md5_block(h, ring[j][i]);
+      }
+  }
+  for (int64_t b = ngroups * G; b < nfull; b++) {
+    uint32_t m[16];
+    load_block<NT>(p + b * 64, m);
+    md5_block(h, m);
+  }
+}
+
+struct Md5Args {
+  Md5Region r[kMaxMd5Regions];
+  int64_t lane_end[kMaxMd5Regions];  // prefix sums of nchunks * nstripes
+  int nregions;
+};
+
+// one lane per chunk over the concatenated regions
+template <int D, int G, bool NT>
+__global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
-  if (c >= total) return;
-  const int64_t s = c / nchunks;
-  const uint8_t *p = base + s * stripe_stride + (c - s * nchunks) * chunk_stride;
+  if (c >= args.lane_end[args.nregions - 1]) return;
+  int ri = 0;
+#pragma unroll
+  for (int i = 0; i < kMaxMd5Regions - 1; i++)
+    if (i < args.nregions - 1 && c >= args.lane_end[i]) ri = i + 1;
+  const Md5Region &rg = args.r[ri];
+  const int64_t cl = c - (ri ? args.lane_end[ri - 1] : 0);
+  const int64_t s = cl / rg.nchunks, ci = cl - s * rg.nchunks;
+  const uint8_t *p = rg.base + s * rg.stripe_stride + ci * rg.chunk_stride;
+  const int64_t len = rg.len;
+  const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
   const int64_t nfull = len / 64;
   uint32_t m[16];
   if (aligned) {
-    if (nfull > 0) md5_stream<D, NT>(p, nfull, h);
+    if (nfull > 0) md5_stream<D, G, NT>(p, nfull, h);
   } else {
     for (int64_t b = 0; b < nfull; b++) {
 #pragma unroll
@@ -172,45 +199,59 @@ __global__ __launch_bounds__(64) void k_md5(const uint8_t *base, int64_t chunk_s
     }
     md5_block(h, m);
   }
-  uint32_t *o = reinterpret_cast<uint32_t *>(digests + c * 16);
+  uint32_t *o = reinterpret_cast<uint32_t *>(rg.digests + s * rg.dig_stripe_stride + ci * 16);
   o[0] = h[0];
   o[1] = h[1];
   o[2] = h[2];
   o[3] = h[3];
 }
 
-int md5_depth() {
-  static const int d = [] {
-    const char *e = getenv("NXEC_MD5_DEPTH");  // tuning override: prefetch ring depth 2..4
-    const int v = e ? atoi(e) : 3;
-    return v >= 2 && v <= 4 ? v : 3;
-  }();
-  return d;
+// Kernel variant (prefetch ring depth D, group G blocks, nontemporal loads):
+// default D=2 G=8 cached (512-byte runs per lane, 12.6 ms for 57 344 1-MiB chunks); NXEC_MD5_CFG="D,G,NT" overrides for tuning
+// (tools/gpu_md5_tune.sh).  Cached loads: a lane reads each 64-byte block as
+// four 16-byte loads and nontemporal loads refetch the line for each (3x
+// slower, profiles/r01_md5_tune.log).
+using Md5Kernel = void (*)(const Md5Args);
+
+template <int D, int G>
+Md5Kernel pick_nt(bool nt) {
+  return nt ? k_md5<D, G, true> : k_md5<D, G, false>;
 }
 
-bool md5_nontemporal() {
-  static const bool nt = [] {
-    const char *e = getenv("NXEC_MD5_NT");  // tuning override: 0 = cached loads
-    return !(e && e[0] == '0');
+Md5Kernel md5_kernel() {
+  static const Md5Kernel k = [] {
+    int d = 2, g = 8, nt = 0;
+    if (const char *e = getenv("NXEC_MD5_CFG")) sscanf(e, "%d,%d,%d", &d, &g, &nt);
+    if (d == 2 && g == 1) return pick_nt<2, 1>(nt);
+    if (d == 4 && g == 1) return pick_nt<4, 1>(nt);
+    if (d == 2 && g == 2) return pick_nt<2, 2>(nt);
+    if (d == 3 && g == 2) return pick_nt<3, 2>(nt);
+    if (d == 3 && g == 4) return pick_nt<3, 4>(nt);
+    if (d == 2 && g == 8) return pick_nt<2, 8>(nt);
+    if (d == 2 && g == 4) return pick_nt<2, 4>(nt);
+    return pick_nt<2, 8>(nt);
   }();
-  return nt;
+  return k;
 }
 
 }  // namespace
 
-int launch_md5(const uint8_t *base, int64_t chunk_stride, int64_t stripe_stride, int nchunks, int64_t len,
-               int64_t nstripes, uint8_t *digests, void *stream) {
-  const int64_t total = static_cast<int64_t>(nchunks) * nstripes;
-  if (total <= 0) return NXEC_OK;
-  const bool aligned = (reinterpret_cast<uintptr_t>(base) % 16 == 0) && (chunk_stride % 16 == 0) &&
-                       (stripe_stride % 16 == 0);
+int launch_md5(const Md5Region *regions, int nregions, void *stream) {
+  Md5Args args{};
+  int64_t total = 0;
+  int nr = 0;
+  for (int i = 0; i < nregions && i < kMaxMd5Regions; i++) {
+    const int64_t lanes = static_cast<int64_t>(regions[i].nchunks) * regions[i].nstripes;
+    if (lanes <= 0) continue;  // empty regions are dropped
+    args.r[nr] = regions[i];
+    total += lanes;
+    args.lane_end[nr++] = total;
+  }
+  if (nr == 0) return NXEC_OK;
+  args.nregions = nr;
   const int64_t blocks = (total + 63) / 64;
-  const int d = md5_depth();
-  const bool nt = md5_nontemporal();
-  auto kern = nt ? (d == 2 ? k_md5<2, true> : d == 4 ? k_md5<4, true> : k_md5<3, true>)
-                 : (d == 2 ? k_md5<2, false> : d == 4 ? k_md5<4, false> : k_md5<3, false>);
-  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream), base,
-                     chunk_stride, stripe_stride, nchunks, len, total, digests, aligned ? 1 : 0);
+  const Md5Kernel kern = md5_kernel();
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream), args);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_md5: %s", hipGetErrorString(e));
 }

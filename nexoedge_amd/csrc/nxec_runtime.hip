@@ -47,6 +47,8 @@ static int hip_err(hipError_t e, const char *what) {
                    hipGetErrorString(e));
 }
 
+static int hip_check(hipError_t e, const char *what) { return e == hipSuccess ? NXEC_OK : hip_err(e, what); }
+
 #define NXEC_HIP(call)                           \
   do {                                           \
     hipError_t e_ = (call);                      \
@@ -407,7 +409,96 @@ int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_
     return set_error(NXEC_ERR_INVALID, "nxec_md5_chunks: invalid arguments");
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
-  return launch_md5(d_base, chunk_stride, stripe_stride, nchunks, len, nstripes, d_digests, pick_stream(ctx, stream));
+  const Md5Region r{d_base, chunk_stride, stripe_stride, len, nstripes, d_digests, int64_t(nchunks) * 16, nchunks};
+  return launch_md5(&r, 1, pick_stream(ctx, stream));
+}
+
+int nxec_object_layout(int n, int k, int64_t length, int64_t max_chunk_size, int64_t *nstripes,
+                       int64_t *full_stripes, int64_t *last_chunk_size) {
+  if (!valid_nk(n, k) || length < 0 || max_chunk_size <= 0 || !nstripes || !full_stripes || !last_chunk_size)
+    return set_error(NXEC_ERR_INVALID, "nxec_object_layout: invalid arguments");
+  const int64_t stripe_data = max_chunk_size * k;  // getMaxDataSizePerStripe (chunk_manager.cc:1395-1400)
+  *full_stripes = length / stripe_data;
+  const int64_t rem = length - *full_stripes * stripe_data;
+  *nstripes = *full_stripes + (rem > 0 ? 1 : 0);
+  *last_chunk_size = rem > 0 ? (rem + k - 1) / k : (*full_stripes > 0 ? max_chunk_size : 0);  // rs.cc:52-55
+  return NXEC_OK;
+}
+
+int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_object, int64_t length,
+                       int64_t max_chunk_size, unsigned char *d_parity, unsigned char *d_tail, unsigned char *d_md5,
+                       void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  int64_t ns = 0, nf = 0, cs_last = 0;
+  int rc = nxec_object_layout(n, k, length, max_chunk_size, &ns, &nf, &cs_last);
+  if (rc) return rc;
+  if (ns == 0) return NXEC_OK;
+  const int p = n - k;
+  const int64_t M = max_chunk_size;
+  const bool tail = ns > nf;
+  if (!d_object || (p > 0 && !d_parity) || (tail && !d_tail))
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_object: null buffer");
+  rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);
+  const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
+  // full stripes: data chunks are read in place from the object (no copy of
+  // rs.cc:80), parity chunk (s, i) at d_parity + (s*p + i)*M
+  if (nf > 0 && p > 0) {
+    rc = nxec_stripes_mul(ctx, p, k, prow, d_object, nullptr, M, k * M, d_parity, nullptr, M, p * M, nullptr, M, nf,
+                          st);
+    if (rc) return rc;
+  }
+  const unsigned char *tail_src = d_object + nf * k * M;
+  const int64_t rem = length - nf * k * M;
+  if (tail) {  // last stripe: zero-padded to k * cs_last (encodeFile's realloc+memset, chunk_manager.cc:390-399)
+    rc = hip_check(hipMemcpyAsync(d_tail, tail_src, rem, hipMemcpyDeviceToDevice, st), "tail copy");
+    if (!rc && k * cs_last > rem)
+      rc = hip_check(hipMemsetAsync(d_tail + rem, 0, k * cs_last - rem, st), "tail pad");
+    if (!rc && p > 0)
+      rc = nxec_stripes_mul(ctx, p, k, prow, d_tail, nullptr, cs_last, k * cs_last, d_parity + nf * p * M, nullptr, M,
+                            p * M, nullptr, cs_last, 1, st);
+    if (rc) return rc;
+  }
+  if (!d_md5) return NXEC_OK;
+  // per-chunk MD5 (writeFileStripe -> Chunk::computeMD5, chunk_manager.cc:175): one launch over
+  // full-stripe data, full-stripe parity, tail data, tail parity; digests [s][n][16]
+  const int64_t ds = int64_t(n) * 16;
+  const Md5Region r[4] = {
+      {d_object, M, k * M, M, nf, d_md5, ds, k},
+      {d_parity, M, p * M, M, nf, d_md5 + int64_t(k) * 16, ds, p},
+      {d_tail, cs_last, k * cs_last, cs_last, tail ? 1 : 0, d_md5 + nf * ds, ds, k},
+      {d_parity + nf * p * M, M, p * M, cs_last, tail ? 1 : 0, d_md5 + nf * ds + int64_t(k) * 16, ds, p},
+  };
+  return launch_md5(r, 4, st);
+}
+
+int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                       const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
+                       unsigned char *d_tail, void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  int64_t ns = 0, nf = 0, cs_last = 0;
+  int rc = nxec_object_layout(n, k, length, max_chunk_size, &ns, &nf, &cs_last);
+  if (rc) return rc;
+  if (ns == 0) return NXEC_OK;
+  const int64_t M = max_chunk_size;
+  const bool tail = ns > nf;
+  if (!d_chunks || !d_object || (tail && !d_tail)) return set_error(NXEC_ERR_INVALID, "nxec_decode_object: null buffer");
+  hipStream_t st = pick_stream(ctx, stream);
+  // full stripes straight into the object: data chunk j of stripe s at s*k*M + j*M
+  if (nf > 0) {
+    rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks, M, n * M, d_object, M, k * M, M, nf, st);
+    if (rc) return rc;
+  }
+  if (!tail) return NXEC_OK;
+  // last stripe: chunks of cs_last bytes in the same slots; decode to scratch, keep the unpadded bytes
+  rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks + nf * n * M, M, n * M, d_tail, cs_last,
+                              k * cs_last, cs_last, 1, st);
+  if (rc) return rc;
+  const int64_t rem = length - nf * k * M;
+  return hip_check(hipMemcpyAsync(d_object + nf * k * M, d_tail, rem, hipMemcpyDeviceToDevice, st), "tail copy");
 }
 
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,

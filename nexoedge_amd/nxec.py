@@ -90,6 +90,14 @@ def _groups(groups: Sequence[Sequence[int]]):
     return (o, c), op, cp
 
 
+def object_layout(n: int, k: int, length: int, max_chunk_size: int):
+    """(nstripes, full_stripes, last_chunk_size) of an object (nxec_object_layout)."""
+    ns, nf, cl = C.c_int64(), C.c_int64(), C.c_int64()
+    check(lib.nxec_object_layout(n, k, length, max_chunk_size, C.byref(ns), C.byref(nf), C.byref(cl)),
+          "nxec_object_layout")
+    return ns.value, nf.value, cl.value
+
+
 def car_plan(n: int, k: int, failed: int, groups: Sequence[Sequence[int]]):
     """CAR repair plan (chunk_manager.cc:929-986) -> list of (chunk_ids, coeffs) per agent sub-group."""
     keep, op, cp = _groups(groups)
@@ -306,6 +314,19 @@ class Context:
                    digests: int, stream=None) -> None:
         check(lib.nxec_md5_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride, nchunks,
                                   length, nstripes, C.c_void_p(int(digests)), stream), "nxec_md5_chunks")
+
+    def encode_object(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int, tail=None,
+                      md5=None, stream=None) -> None:
+        check(lib.nxec_encode_object(C.c_void_p(self.ptr), n, k, C.c_void_p(int(obj)), length, max_chunk_size,
+                                     C.c_void_p(int(parity)), C.c_void_p(int(tail) if tail else None),
+                                     C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_object")
+
+    def decode_object(self, n: int, k: int, failed: Sequence[int], chunks: int, length: int, max_chunk_size: int,
+                      obj: int, tail=None, stream=None) -> None:
+        f, fp = _i32(failed)
+        check(lib.nxec_decode_object(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(chunks)), length,
+                                     max_chunk_size, C.c_void_p(int(obj)), C.c_void_p(int(tail) if tail else None),
+                                     stream), "nxec_decode_object")
 
     def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
                              batch_stripes: int = 0) -> None:

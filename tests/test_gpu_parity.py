@@ -406,3 +406,50 @@ def test_md5_after_encode_full_batch(gpu_ctx):
             assert got[s, c].tobytes().hex() == hashlib.md5(h[c].tobytes()).hexdigest()
     buf.free()
     dg.free()
+
+
+# ------------------------------------------------------------ object entry (§8f.1)
+@pytest.mark.parametrize("n,k,M,length", [
+    (6, 4, 65536, 3 * 4 * 65536),          # full stripes only
+    (6, 4, 65536, 3 * 4 * 65536 + 5000),   # + ragged last stripe
+    (14, 10, 4096, 10 * 4096 * 7 + 1),     # last stripe of 1-byte chunks
+    (9, 6, 1000, 777),                     # one partial stripe, unaligned chunk size
+    (16, 12, 65536, 12 * 65536 * 2 + 12 * 4096),
+])
+def test_encode_decode_object(gpu_ctx, n, k, M, length):
+    """Batched write path: nxec_encode_object == per-stripe RSCode::encode of the
+    stripes proxy_file_ops.cc would form (oracle), MD5 of every chunk == hashlib;
+    read path: nxec_decode_object with n-k erasures returns the object bytes."""
+    import hashlib
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    p = n - k
+    obj = fill_bytes(length, length + n)
+    ob = up(obj)
+    par = nxec.DeviceBuffer(max(ns * p * M, 1))
+    tail = nxec.DeviceBuffer(k * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, tail.ptr, md5.ptr)
+    gpu_ctx.sync()
+    hp = par.download().reshape(ns, p, M) if ns * p * M else None
+    dg = md5.download().reshape(ns, n, 16)
+    chunks = np.zeros((ns, n, M), dtype=np.uint8)
+    for s in range(ns):
+        cs = M if s < nf else cl
+        sd = np.zeros(k * cs, dtype=np.uint8)
+        piece = obj[s * k * M: s * k * M + k * cs]
+        sd[:len(piece)] = piece
+        st = oracle.rs_encode(n, k, sd, cs)
+        for i in range(p):
+            assert np.array_equal(hp[s, i, :cs], st[k + i]), (s, i)
+        for c in range(n):
+            assert dg[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
+            chunks[s, c, :cs] = st[c]
+    failed = list(range(p)) if n > k else []  # lose data chunks: a real decode
+    chunks[:, failed] = 0
+    cb = up(chunks)
+    out = nxec.DeviceBuffer(length)
+    gpu_ctx.decode_object(n, k, failed, cb.ptr, length, M, out.ptr, tail.ptr)
+    gpu_ctx.sync()
+    assert np.array_equal(out.download(), obj)
+    for b in (ob, par, tail, md5, cb, out):
+        b.free()

@@ -1,6 +1,7 @@
 """libnxec's host planning math (section 1 and rs_plan of include/nxec.h)
 against the reference's golden vectors.  These are host-side matrix routines
 (no GPU), exactly like rs.cc:26,196,219,290,316 run on the host."""
+import pytest
 import numpy as np
 
 from nexoedge_amd import nxec
@@ -101,3 +102,16 @@ def test_car_plan_unordered_racks_and_errors():
     assert [ch for ch, _ in subs][:2] == [[12], [3, 1, 0, 2]]  # rack order and in-rack order kept
     with pytest.raises(nxec.NxecError):
         nxec.car_plan(n, k, 5, [[0, 1, 2]])  # racks do not cover the inputs
+
+
+@pytest.mark.parametrize("n,k,length,M,want", [
+    (14, 10, 0, 1 << 20, (0, 0, 0)),
+    (14, 10, 10 << 20, 1 << 20, (1, 1, 1 << 20)),
+    (14, 10, (30 << 20) + 1, 1 << 20, (4, 3, 1)),
+    (6, 4, 4 << 20, 1 << 20, (1, 1, 1 << 20)),
+    (6, 4, 4097, 4096, (1, 0, 1025)),
+    (16, 12, 12 * 4096 * 5 + 13, 4096, (6, 5, 2)),
+])
+def test_object_layout(n, k, length, M, want):
+    """Stripe split of proxy_file_ops.cc:557-666 and chunk size of rs.cc:52-55."""
+    assert nxec.object_layout(n, k, length, M) == want
