@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-ref-stripes", type=int, default=96, help="stripes for the (slow) reference base-C leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D->encode->D2H pipeline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
-    ap.add_argument("--workload", choices=["rs10_4", "repair12", "mixed16", "write14"], default="rs10_4",
+    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object"]), default="rs10_4",
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
@@ -255,7 +255,40 @@ def wl_write14(args, ctx, stream, rank):
                     [buf, dig], f"k_mul_vec<K={k},R=16> (encode launch)", ns)
 
 
-WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14}
+def wl_object(args, ctx, stream, rank):
+    """Object-level write and read: nxec_encode_object over an
+    object of `stripes` full RS(10,4) stripes (data chunks read in place,
+    parity + MD5 of all n chunks per stripe, chunk_manager.cc:99-175,369-452),
+    and nxec_decode_object of the stored chunks with 4 data chunks lost
+    (decodeFile, chunk_manager.cc:738-800) back into a contiguous object."""
+    n, k, M, ns = args.n, args.k, args.chunk, args.stripes
+    p = n - k
+    length = ns * k * M
+    obj = nxec.DeviceBuffer(length)
+    obj.fill_random(0xD00D + rank)
+    par = nxec.DeviceBuffer(ns * p * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    chunks = nxec.DeviceBuffer(ns * n * M)
+    chunks.fill_random(0xF00D + rank)
+    ctx.rs_encode(n, k, chunks.ptr, M, n * M, M, ns, stream)
+    out = nxec.DeviceBuffer(length)
+    failed = list(range(min(4, p)))
+    ops = [
+        ("write_encode_object_md5", lambda i: ctx.encode_object(n, k, obj.ptr, length, M, par.ptr, None, md5.ptr, stream),
+         2 * ns * n * M),
+        ("read_decode_object", lambda i: ctx.decode_object(n, k, failed, chunks.ptr, length, M, out.ptr, None, stream),
+         2 * ns * k * M),
+    ]
+    config = {"workload": f"object of {ns} RS({n},{k}) stripes ({length >> 30} GiB), {M >> 10} KiB chunks: write = "
+                          f"encode_object + MD5 of all chunks, read = decode_object with chunks {failed} lost",
+              "stripes_per_gpu": ns, "chunk_bytes": M,
+              "byte_accounting": "write: encode n*cs + MD5 n*cs per stripe; read: full-output decode 2k*cs per stripe"}
+    return Workload("object", "GiB/s object write (encode+MD5) + read (decode), RS(10,4), 1 MiB chunks, device-resident",
+                    config, ops, [obj, par, md5, chunks, out], "encode_object (encode + MD5 launches)", ns)
+
+
+WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14,
+             "object": wl_object}
 
 
 def main():

@@ -226,6 +226,29 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream);
 
+/* ---- Agent coding service: the agent's two compute steps,
+ * batched over many requests.  Each request is CodingUtils::encode
+ * (coding_util.hh:25-31) of `ninputs` host chunks by a noutputs x ninputs
+ * matrix: the ENC_CHUNK_REQ partial encode (ContainerManager::
+ * getEncodedChunks, container_manager.cc:221-258: 1 x g row) or the
+ * RPR_CHUNK_REQ repair (agent.cc:240-415: all-ones 1 x G for CAR, the
+ * proxy's e x k matrix otherwise), plus the MD5 of every output
+ * (agent.cc:342) when md5 != NULL.  Requests with the same shape and matrix
+ * run as one kernel pass; staging is pinned and double-buffered so the host
+ * gather of batch i+1 overlaps the GPU work of batch i.  batch_bytes bounds
+ * the staging per batch (<= 0: 256 MiB).  Synchronous; thread-safe. */
+typedef struct nxec_agent_req {
+  int ninputs;
+  int noutputs;
+  const unsigned char *matrix;        /* noutputs x ninputs, row-major */
+  const unsigned char *const *inputs; /* ninputs host chunks of chunk_size bytes */
+  unsigned char *const *outputs;      /* noutputs host buffers of chunk_size bytes */
+  unsigned char *md5;                 /* noutputs x 16 digest bytes, or NULL */
+} nxec_agent_req;
+
+int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
+                            int64_t batch_bytes);
+
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU
  *    framework can drive section 3.  Thin wrappers over the HIP runtime.

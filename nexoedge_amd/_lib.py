@@ -60,6 +60,7 @@ _PROTOS = {
     "nxec_object_layout": (C.c_int, [C.c_int, C.c_int, i64, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, vp, vp]),
     "nxec_decode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp]),
+    "nxec_agent_encode_batch": (C.c_int, [vp, vp, C.c_int, i64, i64]),
     "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
     "nxec_rs_plan": (C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
     "nxec_rs_decode_matrix": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp]),
@@ -88,6 +89,12 @@ _PROTOS = {
     "nxec_checksum": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), vp]),
     "nxec_describe_launch": (C.c_int, [vp, C.c_int, C.c_int, i64, i64, C.c_char_p, C.c_int]),
 }
+
+class AgentReq(C.Structure):
+    """struct nxec_agent_req of include/nxec.h"""
+    _fields_ = [("ninputs", C.c_int), ("noutputs", C.c_int), ("matrix", vp), ("inputs", vp), ("outputs", vp),
+                ("md5", vp)]
+
 
 for _name, (_res, _args) in _PROTOS.items():
     _fn = getattr(lib, _name)

@@ -227,7 +227,6 @@ Md5Kernel md5_kernel() {
     if (d == 2 && g == 2) return pick_nt<2, 2>(nt);
     if (d == 3 && g == 2) return pick_nt<3, 2>(nt);
     if (d == 3 && g == 4) return pick_nt<3, 4>(nt);
-    if (d == 2 && g == 8) return pick_nt<2, 8>(nt);
     if (d == 2 && g == 4) return pick_nt<2, 4>(nt);
     return pick_nt<2, 8>(nt);
   }();

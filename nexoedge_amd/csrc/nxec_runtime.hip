@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -499,6 +500,117 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
   if (rc) return rc;
   const int64_t rem = length - nf * k * M;
   return hip_check(hipMemcpyAsync(d_object + nf * k * M, d_tail, rem, hipMemcpyDeviceToDevice, st), "tail copy");
+}
+
+namespace {
+
+// One batch of same-shape agent requests in a staging slot: [B][ninputs][stride]
+// inputs, [B][noutputs][stride] outputs, [B][noutputs][16] digests.
+struct AgentBatch {
+  Slot *slot = nullptr;
+  std::vector<int> reqs;  // request indices staged in this slot (outputs pending)
+  size_t out_off = 0, md5_off = 0;
+  int64_t stride = 0;
+};
+
+int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
+  if (b.reqs.empty()) return NXEC_OK;
+  NXEC_HIP(hipStreamSynchronize(b.slot->stream));
+  const nxec_agent_req &r0 = reqs[b.reqs[0]];
+  for (size_t i = 0; i < b.reqs.size(); i++) {
+    const nxec_agent_req &r = reqs[b.reqs[i]];
+    for (int o = 0; o < r0.noutputs; o++)
+      std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * r0.noutputs + o) * b.stride, cs);
+    if (r.md5) std::memcpy(r.md5, b.slot->h + b.md5_off + i * r0.noutputs * 16, size_t(r0.noutputs) * 16);
+  }
+  b.reqs.clear();
+  return NXEC_OK;
+}
+
+}  // namespace
+
+int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
+                            int64_t batch_bytes) {
+  if (!ctx || nreqs < 0 || chunk_size < 0 || (nreqs > 0 && !reqs))
+    return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: invalid arguments");
+  for (int i = 0; i < nreqs; i++) {
+    const nxec_agent_req &r = reqs[i];
+    if (r.ninputs < 1 || r.ninputs > NXEC_MAX_K || r.noutputs < 1 || r.noutputs > NXEC_MAX_N || !r.matrix ||
+        !r.inputs || !r.outputs)
+      return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: request %d malformed", i);
+  }
+  if (nreqs == 0 || chunk_size == 0) return NXEC_OK;
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  // group requests by (ninputs, noutputs, matrix): one kernel pass per batch of a group
+  std::map<std::string, std::vector<int>> groups;
+  for (int i = 0; i < nreqs; i++) {
+    const nxec_agent_req &r = reqs[i];
+    std::string key(reinterpret_cast<const char *>(&r.ninputs), sizeof(int));
+    key.append(reinterpret_cast<const char *>(&r.noutputs), sizeof(int));
+    key.append(reinterpret_cast<const char *>(r.matrix), size_t(r.ninputs) * r.noutputs);
+    groups[key].push_back(i);
+  }
+  const int64_t stride = (chunk_size + 15) / 16 * 16;
+  if (batch_bytes <= 0) batch_bytes = int64_t(256) << 20;
+  AgentBatch slots[2];
+  int cur = 0;
+  rc = NXEC_OK;
+  for (auto &kv : groups) {
+    const std::vector<int> &ids = kv.second;
+    const nxec_agent_req &r0 = reqs[ids[0]];
+    const int ni = r0.ninputs, no = r0.noutputs;
+    const int64_t per = (int64_t(ni) + no) * stride + int64_t(no) * 16;
+    const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));
+    for (size_t first = 0; first < ids.size() && rc == NXEC_OK; first += B) {
+      const int64_t nb = std::min<int64_t>(B, int64_t(ids.size() - first));
+      AgentBatch &b = slots[cur];
+      cur ^= 1;
+      if ((rc = agent_finish(reqs, chunk_size, b))) break;  // this slot's previous batch
+      if (!b.slot && (rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
+      if (b.slot->cap < size_t(B * per)) {  // grown group: re-acquire a larger slot
+        release_slot(ctx, b.slot);
+        b.slot = nullptr;
+        if ((rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
+      }
+      const size_t in_bytes = size_t(nb) * ni * stride;
+      b.stride = stride;
+      b.out_off = in_bytes;
+      b.md5_off = in_bytes + size_t(nb) * no * stride;
+      for (int64_t i = 0; i < nb; i++) {  // gather the request's chunks into pinned staging
+        const nxec_agent_req &r = reqs[ids[first + i]];
+        for (int j = 0; j < ni; j++) std::memcpy(b.slot->h + (i * ni + j) * stride, r.inputs[j], chunk_size);
+        b.reqs.push_back(ids[first + i]);
+      }
+      hipStream_t st = b.slot->stream;
+      uint8_t *d_in = b.slot->d, *d_out = b.slot->d + b.out_off, *d_md5 = b.slot->d + b.md5_off;
+      bool any_md5 = false;
+      for (int64_t i = 0; i < nb; i++) any_md5 |= reqs[ids[first + i]].md5 != nullptr;
+      if ((rc = hip_check(hipMemcpyAsync(d_in, b.slot->h, in_bytes, hipMemcpyHostToDevice, st), "agent H2D"))) break;
+      // CodingUtils::encode (container_manager.cc:251, agent.cc:339) for the whole batch
+      rc = nxec_stripes_mul(ctx, no, ni, r0.matrix, d_in, nullptr, stride, ni * stride, d_out, nullptr, stride,
+                            no * stride, nullptr, chunk_size, nb, st);
+      if (rc) break;
+      if (any_md5) {  // Chunk::computeMD5 of the outputs (agent.cc:342)
+        const Md5Region reg{d_out, stride, no * stride, chunk_size, nb, d_md5, int64_t(no) * 16, no};
+        if ((rc = launch_md5(&reg, 1, st))) break;
+      }
+      rc = hip_check(hipMemcpyAsync(b.slot->h + b.out_off, d_out, size_t(nb) * (no * stride + (any_md5 ? no * 16 : 0)),
+                                    hipMemcpyDeviceToHost, st),
+                     "agent D2H");
+      if (rc) break;
+    }
+    if (rc) break;
+  }
+  for (AgentBatch &b : slots) {
+    if (b.slot) {
+      int rc2 = rc ? NXEC_OK : agent_finish(reqs, chunk_size, b);
+      if (rc) (void)hipStreamSynchronize(b.slot->stream);
+      if (!rc) rc = rc2;
+      release_slot(ctx, b.slot);
+    }
+  }
+  return rc;
 }
 
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,

@@ -12,7 +12,7 @@ from typing import Iterable, Optional, Sequence
 
 import numpy as np
 
-from ._lib import NXEC_OK, NxecError, check, lib
+from ._lib import NXEC_OK, AgentReq, NxecError, check, lib
 
 
 def _u8(a: np.ndarray) -> C.c_void_p:
@@ -327,6 +327,21 @@ class Context:
         check(lib.nxec_decode_object(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(chunks)), length,
                                      max_chunk_size, C.c_void_p(int(obj)), C.c_void_p(int(tail) if tail else None),
                                      stream), "nxec_decode_object")
+
+    def agent_encode_batch(self, reqs, chunk_size: int, batch_bytes: int = 0) -> None:
+        """nxec_agent_encode_batch: reqs = [(matrix (no x ni), inputs [ni arrays], outputs [no arrays],
+        md5 (no x 16 uint8 array) or None)], host numpy buffers of chunk_size bytes."""
+        keep = []
+        arr = (AgentReq * max(len(reqs), 1))()
+        for i, (m, ins, outs, md5) in enumerate(reqs):
+            m = np.ascontiguousarray(m, dtype=np.uint8)
+            ip = (C.c_void_p * len(ins))(*[a.ctypes.data for a in ins])
+            op = (C.c_void_p * len(outs))(*[a.ctypes.data for a in outs])
+            keep += [m, ip, op]
+            arr[i] = AgentReq(len(ins), len(outs), m.ctypes.data, C.cast(ip, C.c_void_p), C.cast(op, C.c_void_p),
+                                   md5.ctypes.data if md5 is not None else None)
+        check(lib.nxec_agent_encode_batch(C.c_void_p(self.ptr), arr, len(reqs), chunk_size, batch_bytes),
+              "nxec_agent_encode_batch")
 
     def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
                              batch_stripes: int = 0) -> None:

@@ -453,3 +453,39 @@ def test_encode_decode_object(gpu_ctx, n, k, M, length):
     assert np.array_equal(out.download(), obj)
     for b in (ob, par, tail, md5, cb, out):
         b.free()
+
+
+# ------------------------------------------------------------ agent service (§8f.3)
+@pytest.mark.parametrize("batch_bytes", [0, 3 * 8192])
+def test_agent_encode_batch(gpu_ctx, batch_bytes):
+    """Batched agent compute: ENC_CHUNK_REQ partial encodes (1 x g rows of the
+    repair matrix, container_manager.cc:251), CAR RPR XOR of partials
+    (agent.cc:291,339) and non-CAR RPR e x k repairs, interleaved; outputs ==
+    oracle CodingUtils::encode, digests == hashlib.  A small batch_bytes forces
+    many double-buffered batches."""
+    import hashlib
+    rng = np.random.default_rng(7 + batch_bytes)
+    cs = 5000  # not a multiple of 16: padded staging stride + byte tails
+    n, k = 16, 12
+    reqs, want = [], []
+    for t in range(24):
+        kind = t % 3
+        if kind == 0:    # ENC: partial encode of a rack of 4 chunks
+            ids, _, rm = nxec.rs_plan(n, k, [t % n], True)
+            m = rm[:, 4:8]
+        elif kind == 1:  # CAR RPR: XOR of 3 partials
+            m = np.ones((1, 3), dtype=np.uint8)
+        else:            # non-CAR RPR: 2 lost chunks from k inputs
+            f = sorted({t % n, (t * 7 + 3) % n})
+            _, _, m = nxec.rs_plan(n, k, f, True)
+        ins = [rng.integers(0, 256, size=cs, dtype=np.uint8) for _ in range(m.shape[1])]
+        outs = [np.zeros(cs, dtype=np.uint8) for _ in range(m.shape[0])]
+        md5 = np.zeros((m.shape[0], 16), dtype=np.uint8) if t % 4 else None
+        reqs.append((m, ins, outs, md5))
+        want.append(oracle.matmul(m, ins))
+    gpu_ctx.agent_encode_batch(reqs, cs, batch_bytes)
+    for (m, ins, outs, md5), w in zip(reqs, want):
+        for o in range(m.shape[0]):
+            assert np.array_equal(outs[o], w[o])
+            if md5 is not None:
+                assert md5[o].tobytes().hex() == hashlib.md5(w[o].tobytes()).hexdigest()
