@@ -377,6 +377,8 @@ def main():
         result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.name == "rs10_4":
         result["cpu_baseline"] = cpu_baseline(args, args.n, args.k, args.chunk)
+        if args.host_inclusive:
+            result["cpu_baseline"]["write_path_with_md5"] = cpu_write_path(args, args.n, args.k, args.chunk)
     if rank == 0:
         print(json.dumps(result), flush=True)
     for b in wl.buffers:
@@ -401,9 +403,52 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     dt = (time.perf_counter() - t0) / reps
     out = {"encode_GiB_s_(k+p)cs": round(ns * (k + p) * cs / dt / GIB, 2),
            "pcie_bytes_GiB_s": round(ns * (k + p) * cs / dt / GIB, 2), "stripes": ns, "batch": 64}
+    # object write path with MD5 of every chunk (nxec_encode_object_host): the
+    # proxy's writeFileStripe coding work for a host-resident object
+    hm = nxec.PinnedBuffer(ns * n * 16)
+    length = ns * k * cs
+    ctx.encode_object_host(n, k, hd.ptr, length, cs, hp.ptr, hm.ptr)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.encode_object_host(n, k, hd.ptr, length, cs, hp.ptr, hm.ptr)
+    dt = (time.perf_counter() - t0) / reps
+    out["object_write_md5_GiB_s_user_data"] = round(length / dt / GIB, 2)
     hd.free()
     hp.free()
+    hm.free()
     return out
+
+
+def cpu_write_path(args, n, k, cs):
+    """CPU write path of the reference per stripe: encode (SIMD stand-in) + MD5
+    of all n chunks (OpenSSL via hashlib, GIL released), threads over stripes;
+    user-data GiB/s, the same unit as object_write_md5_GiB_s_user_data."""
+    import concurrent.futures as cf
+    import hashlib
+
+    import numpy as np
+
+    import oracle
+
+    p, ns, threads = n - k, min(args.cpu_stripes, 64), args.cpu_threads
+    enc = nxec.gen_rs_matrix(n, k)[k:]
+    data = oracle.fill_bytes(ns * k * cs, 7).reshape(ns, k, cs)
+    parity = np.zeros((ns, p, cs), dtype=np.uint8)
+
+    def work(lo, hi):
+        for s in range(lo, hi):
+            oracle.simd_encode(enc, list(data[s]), list(parity[s]))
+            for c in list(data[s]) + list(parity[s]):
+                hashlib.md5(c).digest()
+
+    bounds = [(ns * t // threads, ns * (t + 1) // threads) for t in range(threads)]
+    with cf.ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda b: work(*b), bounds))
+        dt = time.perf_counter() - t0
+    return {"value": round(ns * k * cs / dt / GIB, 3), "unit": "GiB/s user data", "cores": threads, "kind": "port",
+            "sample": f"{ns} RS({n},{k}) stripes of {cs >> 10} KiB chunks: SIMD encode + hashlib MD5 of all "
+                      f"{n} chunks per stripe, {threads} threads"}
 
 
 if __name__ == "__main__":

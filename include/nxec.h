@@ -226,6 +226,16 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream);
 
+/* Host-inclusive form of nxec_encode_object: the object, parity
+ * ([nstripes][n-k][M]) and digests ([nstripes][n][16], NULL = skip) are in
+ * host memory (pin them -- nxec_host_malloc_pinned / nxec_host_register -- for
+ * full PCIe rate).  Batches of batch_stripes stripes (<= 0: ~1 GiB of chunks)
+ * stream H2D -> encode -> MD5 -> D2H on three concurrent streams.
+ * Synchronous. */
+int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_object, int64_t length,
+                            int64_t max_chunk_size, unsigned char *h_parity, unsigned char *h_md5,
+                            int64_t batch_stripes);
+
 /* ---- Agent coding service: the agent's two compute steps,
  * batched over many requests.  Each request is CodingUtils::encode
  * (coding_util.hh:25-31) of `ninputs` host chunks by a noutputs x ninputs

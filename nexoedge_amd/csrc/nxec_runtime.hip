@@ -684,6 +684,101 @@ int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char
   return NXEC_OK;
 }
 
+int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_object, int64_t length,
+                            int64_t max_chunk_size, unsigned char *h_parity, unsigned char *h_md5,
+                            int64_t batch_stripes) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  int64_t nst = 0, nf = 0, cs_last = 0;
+  int rc = nxec_object_layout(n, k, length, max_chunk_size, &nst, &nf, &cs_last);
+  if (rc) return rc;
+  if (nst == 0) return NXEC_OK;
+  const int p = n - k;
+  const int64_t M = max_chunk_size;
+  if (!h_object || (p > 0 && !h_parity)) return set_error(NXEC_ERR_INVALID, "nxec_encode_object_host: null buffer");
+  rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  // MD5 is chain-bound (~one chunk's hash time per launch whatever the chunk
+  // count), so batches are large and the slots' streams run concurrently
+  if (batch_stripes <= 0) batch_stripes = std::max<int64_t>(1, (int64_t(1) << 30) / (M * n));
+  batch_stripes = std::min(batch_stripes, nst);
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);
+  const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
+  constexpr int kSlots = 3;
+  const size_t dbytes = size_t(batch_stripes) * k * M, pbytes = size_t(batch_stripes) * std::max(p, 1) * M,
+               mbytes = size_t(batch_stripes) * n * 16;
+  uint8_t *dbuf[kSlots] = {}, *pbuf[kSlots] = {}, *mbuf[kSlots] = {};
+  hipStream_t streams[kSlots] = {};
+  auto cleanup = [&]() {
+    for (int i = 0; i < kSlots; i++) {
+      if (streams[i]) {
+        (void)hipStreamSynchronize(streams[i]);
+        (void)hipStreamDestroy(streams[i]);
+      }
+      if (dbuf[i]) (void)hipFree(dbuf[i]);
+      if (pbuf[i]) (void)hipFree(pbuf[i]);
+      if (mbuf[i]) (void)hipFree(mbuf[i]);
+    }
+  };
+  for (int i = 0; i < kSlots; i++) {
+    hipError_t e = hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&dbuf[i]), dbytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&pbuf[i]), pbytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&mbuf[i]), mbytes);
+    if (e != hipSuccess) {
+      cleanup();
+      return hip_err(e, "encode_object_host setup");
+    }
+  }
+  const int64_t ds = int64_t(n) * 16;
+  int64_t b = 0;
+  for (int64_t s0 = 0; s0 < nst && rc == NXEC_OK; s0 += batch_stripes, b++) {
+    const int slot = static_cast<int>(b % kSlots);
+    hipStream_t st = streams[slot];
+    const int64_t nb = std::min(batch_stripes, nst - s0);
+    const int64_t nfull = std::max<int64_t>(0, std::min(nb, nf - s0));  // full stripes in this batch
+    const bool tail = s0 + nb > nf;
+    // data: the full stripes are one contiguous run of the object
+    if (nfull > 0)
+      rc = hip_check(hipMemcpyAsync(dbuf[slot], h_object + s0 * k * M, size_t(nfull) * k * M, hipMemcpyHostToDevice, st),
+                     "H2D");
+    uint8_t *dtail = dbuf[slot] + nfull * k * M;
+    const int64_t rem = length - nf * k * M;
+    if (!rc && tail) {
+      rc = hip_check(hipMemsetAsync(dtail, 0, size_t(k) * cs_last, st), "tail pad");
+      if (!rc) rc = hip_check(hipMemcpyAsync(dtail, h_object + nf * k * M, rem, hipMemcpyHostToDevice, st), "tail H2D");
+    }
+    if (!rc && p > 0 && nfull > 0)
+      rc = nxec_stripes_mul(ctx, p, k, prow, dbuf[slot], nullptr, M, k * M, pbuf[slot], nullptr, M, p * M, nullptr, M,
+                            nfull, st);
+    if (!rc && p > 0 && tail)
+      rc = nxec_stripes_mul(ctx, p, k, prow, dtail, nullptr, cs_last, k * cs_last, pbuf[slot] + nfull * p * M, nullptr,
+                            M, p * M, nullptr, cs_last, 1, st);
+    if (!rc && h_md5) {
+      const Md5Region r[4] = {
+          {dbuf[slot], M, k * M, M, nfull, mbuf[slot], ds, k},
+          {pbuf[slot], M, p * M, M, p > 0 ? nfull : 0, mbuf[slot] + int64_t(k) * 16, ds, p},
+          {dtail, cs_last, k * cs_last, cs_last, tail ? 1 : 0, mbuf[slot] + nfull * ds, ds, k},
+          {pbuf[slot] + nfull * p * M, M, p * M, cs_last, (tail && p > 0) ? 1 : 0,
+           mbuf[slot] + nfull * ds + int64_t(k) * 16, ds, p},
+      };
+      rc = launch_md5(r, 4, st);
+    }
+    if (!rc && p > 0 && nfull > 0)
+      rc = hip_check(hipMemcpyAsync(h_parity + s0 * p * M, pbuf[slot], size_t(nfull) * p * M, hipMemcpyDeviceToHost, st),
+                     "D2H");
+    if (!rc && p > 0 && tail)  // last stripe: first cs_last bytes of each parity slot
+      rc = hip_check(hipMemcpy2DAsync(h_parity + nf * p * M, M, pbuf[slot] + nfull * p * M, M, cs_last, p,
+                                      hipMemcpyDeviceToHost, st),
+                     "tail D2H");
+    if (!rc && h_md5)
+      rc = hip_check(hipMemcpyAsync(h_md5 + s0 * ds, mbuf[slot], size_t(nb) * ds, hipMemcpyDeviceToHost, st), "md5 D2H");
+  }
+  for (int i = 0; i < kSlots && !rc; i++) rc = hip_check(hipStreamSynchronize(streams[i]), "encode_object_host sync");
+  cleanup();
+  return rc;
+}
+
 int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
                         unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out) {
   int ncopy = 0;

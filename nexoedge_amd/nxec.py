@@ -321,6 +321,12 @@ class Context:
                                      C.c_void_p(int(parity)), C.c_void_p(int(tail) if tail else None),
                                      C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_object")
 
+    def encode_object_host(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int,
+                           md5=None, batch_stripes: int = 0) -> None:
+        check(lib.nxec_encode_object_host(C.c_void_p(self.ptr), n, k, C.c_void_p(int(obj)), length, max_chunk_size,
+                                          C.c_void_p(int(parity)), C.c_void_p(int(md5) if md5 else None),
+                                          batch_stripes), "nxec_encode_object_host")
+
     def decode_object(self, n: int, k: int, failed: Sequence[int], chunks: int, length: int, max_chunk_size: int,
                       obj: int, tail=None, stream=None) -> None:
         f, fp = _i32(failed)

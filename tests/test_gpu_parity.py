@@ -489,3 +489,29 @@ def test_agent_encode_batch(gpu_ctx, batch_bytes):
             assert np.array_equal(outs[o], w[o])
             if md5 is not None:
                 assert md5[o].tobytes().hex() == hashlib.md5(w[o].tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("batch", [0, 2])
+def test_encode_object_host_matches_device(gpu_ctx, batch):
+    """Host-inclusive object write (H2D -> encode -> MD5 -> D2H, three streams)
+    == the device-resident nxec_encode_object, ragged last stripe included."""
+    n, k, M = 14, 10, 8192
+    length = 7 * k * M + 12345
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    obj = fill_bytes(length, 5)
+    hpar = np.zeros(ns * (n - k) * M, dtype=np.uint8)
+    hmd5 = np.zeros(ns * n * 16, dtype=np.uint8)
+    gpu_ctx.encode_object_host(n, k, obj.ctypes.data, length, M, hpar.ctypes.data, hmd5.ctypes.data, batch)
+    ob = up(obj)
+    par = nxec.DeviceBuffer(ns * (n - k) * M)
+    tail = nxec.DeviceBuffer(k * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, tail.ptr, md5.ptr)
+    gpu_ctx.sync()
+    dpar = par.download().reshape(ns, n - k, M)
+    hp = hpar.reshape(ns, n - k, M)
+    assert np.array_equal(hp[:nf], dpar[:nf])
+    assert np.array_equal(hp[nf:, :, :cl], dpar[nf:, :, :cl])
+    assert np.array_equal(hmd5, md5.download())
+    for b in (ob, par, tail, md5):
+        b.free()
