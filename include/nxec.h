@@ -84,6 +84,20 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
                         unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out);
 
 /* ---------------------------------------------------------------------------
+ * 2b. The boundary under the names of SURVEY §8b (thin forms of the above,
+ *     coefficient matrices instead of 32-B tables, non-clobbering inverse).
+ * ------------------------------------------------------------------------- */
+/* == nxec_gf_gen_rs_matrix (ISA-L gf_gen_rs_matrix, rs.cc:26) */
+void nxec_gen_rs_matrix(unsigned char *a, int n, int k);
+/* rs.cc:196,290 without ISA-L's clobbering of `in`: 0, or -1 if singular */
+int nxec_invert_matrix(const unsigned char *in, unsigned char *out, int k);
+/* == nxec_ec_init_tables with a const coefficient matrix (ISA-L 32-B layout) */
+void nxec_init_tables(int k, int rows, const unsigned char *coeffs, unsigned char *tbls);
+/* ec_init_tables + ec_encode_data from the rows x k matrix: == nxec_encode_host */
+int nxec_encode_data(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *src,
+                     unsigned char *const *dst);
+
+/* ---------------------------------------------------------------------------
  * 3. Contexts and batched device-resident stripe ops.
  *    Layout: stripe s, chunk c starts at base + s*stripe_stride + c*chunk_stride.
  *    `stream` is a hipStream_t (NULL = the context's stream).  Launches are
@@ -108,6 +122,13 @@ int nxec_stripes_mul(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coef
                      unsigned char *d_dst, const int32_t *dst_idx, int64_t dst_chunk_stride,
                      int64_t dst_stripe_stride, const int32_t *copy_idx, int64_t len, int64_t nstripes,
                      void *stream);
+
+/* SURVEY §8b's nxec_matmul_batch: nxec_stripes_mul with identity index maps
+ * (src chunks 0..k-1, dst chunks 0..rows-1, no copies). */
+int nxec_matmul_batch(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
+                      int64_t src_chunk_stride, int64_t src_stripe_stride, unsigned char *d_dst,
+                      int64_t dst_chunk_stride, int64_t dst_stripe_stride, int64_t len, int64_t nstripes,
+                      void *stream);
 
 /* Gather form for non-contiguous chunks: d_src_ptrs is a DEVICE array of
  * nstripes*k device pointers ([s][j]), d_dst_ptrs of nstripes*rows. */

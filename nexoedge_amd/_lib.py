@@ -33,6 +33,11 @@ _PROTOS = {
     "nxec_gf_gen_rs_matrix": (None, [vp, C.c_int, C.c_int]),
     "nxec_gf_invert_matrix": (C.c_int, [vp, vp, C.c_int]),
     "nxec_ec_init_tables": (None, [C.c_int, C.c_int, vp, vp]),
+    "nxec_gen_rs_matrix": (None, [vp, C.c_int, C.c_int]),
+    "nxec_invert_matrix": (C.c_int, [vp, vp, C.c_int]),
+    "nxec_init_tables": (None, [C.c_int, C.c_int, vp, vp]),
+    "nxec_encode_data": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
+    "nxec_matmul_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, vp, i64, i64, i64, i64, vp]),
     "nxec_ec_encode_data": (None, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
     "nxec_ec_encode_data_status": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
     "nxec_encode_host": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),

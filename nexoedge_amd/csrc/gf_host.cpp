@@ -113,6 +113,18 @@ extern "C" void nxec_ec_init_tables(int k, int rows, unsigned char *a, unsigned 
   }
 }
 
+extern "C" void nxec_gen_rs_matrix(unsigned char *a, int n, int k) { nxec_gf_gen_rs_matrix(a, n, k); }
+
+extern "C" int nxec_invert_matrix(const unsigned char *in, unsigned char *out, int k) {
+  if (!in || !out || k <= 0) return -1;
+  std::vector<unsigned char> tmp(in, in + static_cast<size_t>(k) * k);
+  return nxec_gf_invert_matrix(tmp.data(), out, k);
+}
+
+extern "C" void nxec_init_tables(int k, int rows, const unsigned char *coeffs, unsigned char *tbls) {
+  nxec_ec_init_tables(k, rows, const_cast<unsigned char *>(coeffs), tbls);  // reads coeffs only
+}
+
 namespace nxec {
 
 // Rows that rebuild `targets` from the k inputs whose encode rows are `dm`

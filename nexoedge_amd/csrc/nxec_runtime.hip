@@ -317,6 +317,19 @@ int nxec_stripes_mul(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coef
                           nullptr, dst_idx, dst_chunk_stride, dst_stripe_stride, copy_idx, len, nstripes, stream);
 }
 
+int nxec_matmul_batch(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
+                      int64_t src_chunk_stride, int64_t src_stripe_stride, unsigned char *d_dst,
+                      int64_t dst_chunk_stride, int64_t dst_stripe_stride, int64_t len, int64_t nstripes,
+                      void *stream) {
+  return nxec_stripes_mul(ctx, rows, k, coeffs, d_src, nullptr, src_chunk_stride, src_stripe_stride, d_dst, nullptr,
+                          dst_chunk_stride, dst_stripe_stride, nullptr, len, nstripes, stream);
+}
+
+int nxec_encode_data(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *src,
+                     unsigned char *const *dst) {
+  return nxec_encode_host(len, k, rows, coeffs, src, dst);
+}
+
 int nxec_stripes_mul_ptrs(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs,
                           const unsigned char *const *d_src_ptrs, unsigned char *const *d_dst_ptrs, int64_t len,
                           int64_t nstripes, void *stream) {

@@ -515,3 +515,32 @@ def test_encode_object_host_matches_device(gpu_ctx, batch):
     assert np.array_equal(hmd5, md5.download())
     for b in (ob, par, tail, md5):
         b.free()
+
+
+def test_survey_named_encode_entry_points(gpu_ctx):
+    """nxec_encode_data (host buffers) and nxec_matmul_batch (device batch), the
+    §8b names, agree with the oracle."""
+    import ctypes as C
+
+    from nexoedge_amd._lib import lib
+    rng = np.random.default_rng(11)
+    k, rows, cs, ns = 10, 4, 4096 + 5, 3
+    m = np.ascontiguousarray(nxec.gen_rs_matrix(k + rows, k)[k:])
+    srcs = [rng.integers(0, 256, size=cs, dtype=np.uint8) for _ in range(k)]
+    outs = [np.zeros(cs, dtype=np.uint8) for _ in range(rows)]
+    vp = C.c_void_p
+    assert lib.nxec_encode_data(cs, k, rows, m.ctypes.data, (vp * k)(*[s.ctypes.data for s in srcs]),
+                                (vp * rows)(*[o.ctypes.data for o in outs])) == 0
+    want = oracle.matmul(m, srcs)
+    assert all(np.array_equal(a, b) for a, b in zip(outs, want))
+    data = rng.integers(0, 256, size=(ns, k, cs), dtype=np.uint8)
+    db, pb = up(data), nxec.DeviceBuffer(ns * rows * cs)
+    assert lib.nxec_matmul_batch(vp(gpu_ctx.ptr), rows, k, m.ctypes.data, vp(db.ptr), cs, k * cs, vp(pb.ptr), cs,
+                                 rows * cs, cs, ns, None) == 0
+    gpu_ctx.sync()
+    got = pb.download().reshape(ns, rows, cs)
+    for s in range(ns):
+        w = oracle.matmul(m, list(data[s]))
+        assert all(np.array_equal(got[s, r], w[r]) for r in range(rows))
+    db.free()
+    pb.free()

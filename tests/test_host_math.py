@@ -115,3 +115,32 @@ def test_car_plan_unordered_racks_and_errors():
 def test_object_layout(n, k, length, M, want):
     """Stripe split of proxy_file_ops.cc:557-666 and chunk size of rs.cc:52-55."""
     assert nxec.object_layout(n, k, length, M) == want
+
+
+def test_survey_named_boundary(golden):
+    """The §8b-named forms: nxec_gen_rs_matrix / nxec_init_tables equal the
+    ISA-L-named ones; nxec_invert_matrix equals the golden inverse and leaves
+    its input untouched (unlike ISA-L's gf_invert_matrix)."""
+    import ctypes as C
+
+    from nexoedge_amd._lib import lib
+    for m in golden["matrices"][:10]:
+        n, k = m["n"], m["k"]
+        a = np.zeros(n * k, dtype=np.uint8)
+        lib.nxec_gen_rs_matrix(a.ctypes.data, n, k)
+        assert a.tobytes().hex() == m["hex"]
+    for t in golden["init_tables"][:10]:
+        n, k = t["n"], t["k"]
+        c = np.ascontiguousarray(nxec.gen_rs_matrix(n, k)[k:])
+        tb = np.zeros(c.size * 32, dtype=np.uint8)
+        lib.nxec_init_tables(k, n - k, c.ctypes.data, tb.ctypes.data)
+        assert tb.tobytes().hex() == t["hex"]
+    for t in golden["inverses"][:50]:
+        n, k = t["n"], t["k"]
+        src = np.ascontiguousarray(nxec.gen_rs_matrix(n, k)[t["rows"]])
+        before = src.copy()
+        out = np.zeros_like(src)
+        assert lib.nxec_invert_matrix(src.ctypes.data, out.ctypes.data, k) == 0
+        assert out.tobytes().hex() == t["inv_hex"] and np.array_equal(src, before)
+    z = np.zeros(9, dtype=np.uint8)
+    assert lib.nxec_invert_matrix(z.ctypes.data, np.zeros(9, dtype=np.uint8).ctypes.data, 3) == -1
