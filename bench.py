@@ -75,6 +75,16 @@ def _cpu_run(threads, ns, fn_enc, fn_rec, min_s):
     return reps, enc_s, rec_s
 
 
+def _host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"cpu": model, "nproc": os.cpu_count()}
+
+
 def cpu_baseline(args, n, k, cs):
     """The same encode + (k,e)-recover work on a bounded sample of stripes on the
     host cores (ctypes calls release the GIL; one stripe per call):
@@ -131,6 +141,12 @@ def cpu_baseline(args, n, k, cs):
         "encode_s": round(best[3], 3),
         "decode_s": round(best[4], 3),
     }
+    # one thread of the same port, and the host it ran on
+    nss = min(ns, 16)
+    fe, fr = leg(lambda c, src, dst, lv=best[1]: oracle.simd_encode(c, src, dst, lv))
+    reps, es, rs_ = _cpu_run(1, nss, fe, fr, 1.0)
+    out["single_thread"] = round(reps * nss * stripe_bytes / (es + rs_) / GIB, 3)
+    out["host"] = _host_info()
     if oracle.ref_available():
         ref = oracle.RefISAL()
         nsr = min(ns, args.cpu_ref_stripes)
@@ -331,6 +347,22 @@ def main():
     total_bytes = grp.sum(float(step_bytes * args.steps))
     verified = grp.sum(0.0 if wl.buffers[0].checksum() == sum_before else 1.0) == 0.0
 
+    # on-box copy ceiling: hipMemcpyDtoD of 16 GiB inside the
+    # workload buffer, after the checksum above (it overwrites data)
+    ceiling = None
+    if rank == 0 and wl.buffers[0].nbytes >= (32 << 30):
+        half = 16 << 30
+        e0, e1 = nxec.Event(), nxec.Event()
+        wl.buffers[0].copy_within(half, 0, half, stream)  # warm
+        e0.record(stream)
+        for _ in range(3):
+            wl.buffers[0].copy_within(half, 0, half, stream)
+        e1.record(stream)
+        ctx.sync()
+        ms = e0.elapsed_ms(e1) / 3
+        ceiling = {"d2d_memcpy_GB_s": round(2 * half / (ms * 1e-3) / 1e9, 1),
+                   "note": "hipMemcpyDtoD 16 GiB, read+write bytes counted"}
+
     # per-op event-timed durations on the launch stream
     op_ms = [sum(evs[i][oi].elapsed_ms(evs[i][oi + 1]) for i in range(args.steps)) / args.steps for oi in range(nops)]
 
@@ -370,6 +402,8 @@ def main():
                            "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                     for (name, _, b), ms in zip(wl.ops, op_ms)},
         }
+        if ceiling:
+            result["roofline"]["on_box_ceiling"] = ceiling
         if wl.name == "rs10_4":
             k, cs = args.k, args.chunk
             result["user_data_gib_s"] = round(2 * wl.stripes * k * cs * args.steps * world / elapsed / GIB, 2)

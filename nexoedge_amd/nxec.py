@@ -193,6 +193,11 @@ class DeviceBuffer:
         check(lib.nxec_memset(self.addr(offset), value, n, stream), "memset")
         check(lib.nxec_stream_sync(stream), "sync")
 
+    def copy_within(self, dst_offset: int, src_offset: int, nbytes: int, stream=None) -> None:
+        """Asynchronous device-to-device copy inside this buffer (hipMemcpyAsync)."""
+        assert max(dst_offset, src_offset) + nbytes <= self.nbytes
+        check(lib.nxec_memcpy_d2d(self.addr(dst_offset), self.addr(src_offset), nbytes, stream), "d2d")
+
     def checksum(self, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> int:
         n = self.nbytes - offset if nbytes is None else nbytes
         out = C.c_uint64(0)
