@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-ref-stripes", type=int, default=96, help="stripes for the (slow) reference base-C leg")
     ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D->encode->D2H pipeline")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
-    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object"]), default="rs10_4",
+    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files"]), default="rs10_4",
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
@@ -303,8 +303,40 @@ def wl_object(args, ctx, stream, rank):
                     config, ops, [obj, par, md5, chunks, out], "encode_object (encode + MD5 launches)", ns)
 
 
+def wl_files(args, ctx, stream, rank):
+    """Many files per call (nxec_encode_objects): 4096 files with sizes uniform
+    in [1 B, 2*k*M] (full and ragged last stripes mixed) packed in one arena,
+    encode + MD5 of every chunk.  Bytes = user data + parity written + MD5 reads."""
+    import numpy as np
+
+    n, k, M = args.n, args.k, args.chunk
+    p = n - k
+    rng = np.random.default_rng(1234 + rank)
+    lengths = [int(x) for x in rng.integers(1, 2 * k * M + 1, size=4096)]
+    offs = np.concatenate([[0], np.cumsum([(L + 15) // 16 * 16 for L in lengths])])
+    arena = nxec.DeviceBuffer(int(offs[-1]))
+    arena.fill_random(77 + rank)
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    par = nxec.DeviceBuffer(total * p * M)
+    tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+    md5 = nxec.DeviceBuffer(total * n * 16)
+    ptrs = [arena.ptr + int(o) for o in offs[:-1]]
+    user = sum(lengths)
+    layouts = [nxec.object_layout(n, k, L, M) for L in lengths]
+    chunk_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts)
+    ops = [("encode_objects_md5",
+            lambda i: ctx.encode_objects(n, k, ptrs, lengths, M, par.ptr, tail.ptr, md5.ptr, stream),
+            user + 2 * chunk_bytes * p // n + chunk_bytes)]
+    config = {"workload": f"{len(lengths)} files, sizes uniform in [1 B, {2 * k} MiB], RS({n},{k}) {M >> 10} KiB max "
+                          f"chunks ({total} stripes, {user / 2**30:.1f} GiB user data): encode + MD5 of all chunks",
+              "files": len(lengths), "stripes": total, "user_bytes": user,
+              "byte_accounting": "data read + parity write + MD5 read of every chunk"}
+    return Workload("files", "GiB/s multi-file write (encode+MD5), RS(10,4), 1 MiB max chunk, device-resident",
+                    config, ops, [arena, par, tail, md5], "encode_objects (gather + list + MD5 launches)", total)
+
+
 WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14,
-             "object": wl_object}
+             "object": wl_object, "files": wl_files}
 
 
 def main():

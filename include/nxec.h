@@ -247,6 +247,22 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream);
 
+/* Many objects in one call (the proxy's per-file loop, proxy_file_ops.cc:557-666,
+ * over a batch of files): object o (d_objects[o], a HOST array of device
+ * pointers, lengths[o] bytes) is split as in nxec_object_layout; its stripes
+ * follow the previous objects' in one global stripe order g.  Parity chunk
+ * (g, i) at d_parity + (g*(n-k) + i)*M; digests (NULL = skip) at
+ * d_md5 + g*n*16; the zero-padded data chunks of each object's last stripe
+ * are written to the d_tail arena (size from nxec_objects_layout).  Full
+ * stripes of all objects run as one gather launch, last stripes as one
+ * variable-length launch, every chunk's MD5 as one launch.  Synchronous
+ * (returns when the work is done). */
+int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int64_t max_chunk_size,
+                        int64_t *total_stripes, int64_t *tail_bytes);
+int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
+                        const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
+                        unsigned char *d_tail, unsigned char *d_md5, void *stream);
+
 /* Host-inclusive form of nxec_encode_object: the object, parity
  * ([nstripes][n-k][M]) and digests ([nstripes][n][16], NULL = skip) are in
  * host memory (pin them -- nxec_host_malloc_pinned / nxec_host_register -- for

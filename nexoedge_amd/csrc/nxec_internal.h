@@ -78,6 +78,32 @@ struct Md5Region {
 int launch_md5(const Md5Region *regions, int nregions, void *stream);
 int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
 
+// Variable-length batch (many objects per call): stripe s has its own chunk
+// length and layout.  Source chunk j at src + j*src_cs, output row r at
+// dst + r*dst_cs.  prefix[s] = first 16-byte unit of stripe s (prefix[n] = total).
+struct ListStripe {
+  const uint8_t *src;
+  uint8_t *dst;
+  int64_t len, src_cs, dst_cs;
+};
+// rows x k coefficients (rows <= 4 per pass inside); d_stripes / d_prefix in device memory
+int launch_mul_list(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const int64_t *d_prefix,
+                    int64_t nstripes, int64_t total_units, int num_cus, void *stream);
+// copy item i: dst[0 .. dst_len) = src[0 .. src_len) then zeros (src_len <= dst_len)
+struct PadCopy {
+  const uint8_t *src;
+  uint8_t *dst;
+  int64_t src_len, dst_len;
+};
+int launch_pad_copy(const PadCopy *d_items, int64_t nitems, void *stream);
+// MD5 of a list of chunks: digest of p[0 .. len) to `digest`
+struct Md5Item {
+  const uint8_t *p;
+  int64_t len;
+  uint8_t *digest;
+};
+int launch_md5_list(const Md5Item *d_items, int64_t nitems, void *stream);
+
 }  // namespace nxec
 
 #endif

@@ -380,6 +380,96 @@ __global__ __launch_bounds__(256) void k_mul_bytes(const MulArgs a) {
   }
 }
 
+// --- variable-length batches (many objects per call) ---
+// One launch over stripes of different chunk lengths and layouts.  Work unit =
+// one 16-byte column piece; workgroup b owns the contiguous unit run
+// [b*T/G, (b+1)*T/G), finds its first stripe by binary search over the unit
+// prefix once (thread 0, LDS broadcast), and every thread then advances its
+// own stripe cursor monotonically.  R = 1 packed-row LDS tables; 16-byte
+// vector loads where the piece is complete and aligned, bytes otherwise.
+// Not the throughput path for big objects (their full stripes go through
+// k_mul_vec in gather form); it covers the ragged last stripes.
+struct ListArgs {
+  const ListStripe *stripes;
+  const int64_t *prefix;
+  int64_t nstripes, total;
+  int32_t k, rows, row0;
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];
+};
+
+__global__ __launch_bounds__(256) void k_mul_list(const ListArgs a) {
+  extern __shared__ uint32_t tab[];
+  __shared__ int64_t s_first;
+  const int k = a.k;
+  for (int i = threadIdx.x; i < k * 256; i += blockDim.x) {
+    const int j = i >> 8;
+    uint32_t e = 0;
+    for (int r = 0; r < a.rows; r++) e |= gf_mul_dev(a.coef[r * k + j], static_cast<uint32_t>(i & 255)) << (8 * r);
+    tab[i] = e;
+  }
+  const int64_t u0 = static_cast<int64_t>(blockIdx.x) * a.total / gridDim.x;
+  const int64_t u1 = static_cast<int64_t>(blockIdx.x + 1) * a.total / gridDim.x;
+  if (threadIdx.x == 0) {
+    int64_t lo = 0, hi = a.nstripes - 1;  // last s with prefix[s] <= u0
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (a.prefix[mid] <= u0) lo = mid;
+      else hi = mid - 1;
+    }
+    s_first = lo;
+  }
+  __syncthreads();
+  int64_t s = s_first;
+  const char *tl = reinterpret_cast<const char *>(tab);
+  for (int64_t u = u0 + threadIdx.x; u < u1; u += blockDim.x) {
+    while (a.prefix[s + 1] <= u) s++;
+    const ListStripe st = a.stripes[s];
+    const int64_t off = (u - a.prefix[s]) * 16;
+    const int64_t nb = st.len - off < 16 ? st.len - off : 16;
+    const bool vec = nb == 16 && ((reinterpret_cast<uintptr_t>(st.src) | reinterpret_cast<uintptr_t>(st.dst) |
+                                   static_cast<uint64_t>(st.src_cs) | static_cast<uint64_t>(st.dst_cs) |
+                                   static_cast<uint64_t>(off)) & 15) == 0;
+    uint8_t *drow0 = st.dst + static_cast<int64_t>(a.row0) * st.dst_cs + off;
+    if (vec) {
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+      for (int j = 0; j < k; j++) lookup16<1>(tl + j * 1024, ld_stream(st.src + j * st.src_cs + off), acc);
+      uint32_t o[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
+        const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u), hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
+        const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u), hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+        o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+        o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+        o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+        o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+      }
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++)
+        if (r < a.rows) st_stream(drow0 + r * st.dst_cs, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
+    } else {
+      for (int b = 0; b < nb; b++) {
+        uint32_t acc = 0;
+        for (int j = 0; j < k; j++) acc ^= tab[j * 256 + st.src[j * st.src_cs + off + b]];
+        for (int r = 0; r < a.rows; r++) drow0[r * st.dst_cs + b] = static_cast<uint8_t>(acc >> (8 * r));
+      }
+    }
+  }
+}
+
+// zero-padded copies (the last stripe of each object, chunk_manager.cc:390-399);
+// blockIdx.y-less: item = blockIdx.x / kPadParts, each part a slice of it
+constexpr int kPadParts = 8;
+__global__ __launch_bounds__(256) void k_pad_copy(const PadCopy *items) {
+  const PadCopy it = items[blockIdx.x / kPadParts];
+  const int part = blockIdx.x % kPadParts;
+  const int64_t per = ((it.dst_len + kPadParts - 1) / kPadParts + 15) / 16 * 16;
+  const int64_t b0 = part * per, b1 = b0 + per < it.dst_len ? b0 + per : it.dst_len;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) it.dst[i] = i < it.src_len ? it.src[i] : 0;
+}
+
 __global__ void k_fill(uint8_t *p, int64_t bytes, uint64_t seed) {
   const int64_t words = (bytes + 7) / 8;
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
@@ -576,6 +666,41 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
     if (e != hipSuccess) return hip_fail(e, "launch k_mul_bytes");
   }
   return NXEC_OK;
+}
+
+int launch_mul_list(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const int64_t *d_prefix,
+                    int64_t nstripes, int64_t total_units, int num_cus, void *stream) {
+  if (nstripes <= 0 || total_units <= 0 || rows <= 0) return NXEC_OK;
+  if (k < 1 || k > NXEC_MAX_K) return set_error(NXEC_ERR_INVALID, "k=%d out of range", k);
+  int64_t blocks = (total_units + 255) / 256;
+  if (blocks > static_cast<int64_t>(num_cus) * 8) blocks = static_cast<int64_t>(num_cus) * 8;
+  for (int r0 = 0; r0 < rows; r0 += kMaxRowsPerPass) {
+    ListArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.stripes = d_stripes;
+    a.prefix = d_prefix;
+    a.nstripes = nstripes;
+    a.total = total_units;
+    a.k = k;
+    a.rows = rows - r0 < kMaxRowsPerPass ? rows - r0 : kMaxRowsPerPass;
+    a.row0 = r0;
+    for (int r = 0; r < a.rows; r++)
+      for (int j = 0; j < k; j++) a.coef[r * k + j] = coeffs[static_cast<size_t>(r0 + r) * k + j];
+    hipLaunchKernelGGL(k_mul_list, dim3(static_cast<unsigned>(blocks)), dim3(256), k * 1024,
+                       static_cast<hipStream_t>(stream), a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "launch k_mul_list");
+  }
+  return NXEC_OK;
+}
+
+int launch_pad_copy(const PadCopy *d_items, int64_t nitems, void *stream) {
+  if (nitems <= 0) return NXEC_OK;
+  if (nitems * kPadParts >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "too many pad-copy items");
+  hipLaunchKernelGGL(k_pad_copy, dim3(static_cast<unsigned>(nitems * kPadParts)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), d_items);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_pad_copy");
 }
 
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream) {

@@ -143,22 +143,36 @@ struct Md5Args {
   Md5Region r[kMaxMd5Regions];
   int64_t lane_end[kMaxMd5Regions];  // prefix sums of nchunks * nstripes
   int nregions;
+  const Md5Item *items;  // list mode (items != nullptr): lane c hashes items[c]
+  int64_t nitems;
 };
 
 // one lane per chunk over the concatenated regions
 template <int D, int G, bool NT>
 __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
-  if (c >= args.lane_end[args.nregions - 1]) return;
-  int ri = 0;
+  const uint8_t *p;
+  int64_t len;
+  uint8_t *out;
+  if (args.items) {
+    if (c >= args.nitems) return;
+    const Md5Item it = args.items[c];
+    p = it.p;
+    len = it.len;
+    out = it.digest;
+  } else {
+    if (c >= args.lane_end[args.nregions - 1]) return;
+    int ri = 0;
 #pragma unroll
-  for (int i = 0; i < kMaxMd5Regions - 1; i++)
-    if (i < args.nregions - 1 && c >= args.lane_end[i]) ri = i + 1;
-  const Md5Region &rg = args.r[ri];
-  const int64_t cl = c - (ri ? args.lane_end[ri - 1] : 0);
-  const int64_t s = cl / rg.nchunks, ci = cl - s * rg.nchunks;
-  const uint8_t *p = rg.base + s * rg.stripe_stride + ci * rg.chunk_stride;
-  const int64_t len = rg.len;
+    for (int i = 0; i < kMaxMd5Regions - 1; i++)
+      if (i < args.nregions - 1 && c >= args.lane_end[i]) ri = i + 1;
+    const Md5Region &rg = args.r[ri];
+    const int64_t cl = c - (ri ? args.lane_end[ri - 1] : 0);
+    const int64_t s = cl / rg.nchunks, ci = cl - s * rg.nchunks;
+    p = rg.base + s * rg.stripe_stride + ci * rg.chunk_stride;
+    len = rg.len;
+    out = rg.digests + s * rg.dig_stripe_stride + ci * 16;
+  }
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
   const int64_t nfull = len / 64;
@@ -199,11 +213,8 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
     }
     md5_block(h, m);
   }
-  uint32_t *o = reinterpret_cast<uint32_t *>(rg.digests + s * rg.dig_stripe_stride + ci * 16);
-  o[0] = h[0];
-  o[1] = h[1];
-  o[2] = h[2];
-  o[3] = h[3];
+#pragma unroll
+  for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(h[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
 }
 
 // Kernel variant (prefetch ring depth D, group G blocks, nontemporal loads):
@@ -253,6 +264,18 @@ int launch_md5(const Md5Region *regions, int nregions, void *stream) {
   hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream), args);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_md5: %s", hipGetErrorString(e));
+}
+
+int launch_md5_list(const Md5Item *d_items, int64_t nitems, void *stream) {
+  if (nitems <= 0) return NXEC_OK;
+  Md5Args args{};
+  args.items = d_items;
+  args.nitems = nitems;
+  const int64_t blocks = (nitems + 63) / 64;
+  hipLaunchKernelGGL(md5_kernel(), dim3(static_cast<unsigned>(blocks)), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     args);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_md5 (list): %s", hipGetErrorString(e));
 }
 
 }  // namespace nxec

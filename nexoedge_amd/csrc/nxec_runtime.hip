@@ -489,6 +489,124 @@ int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_obj
   return launch_md5(r, 4, st);
 }
 
+int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int64_t max_chunk_size,
+                        int64_t *total_stripes, int64_t *tail_bytes) {
+  if (!valid_nk(n, k) || nobjects < 0 || (nobjects > 0 && !lengths) || max_chunk_size <= 0 || !total_stripes ||
+      !tail_bytes)
+    return set_error(NXEC_ERR_INVALID, "nxec_objects_layout: invalid arguments");
+  *total_stripes = 0;
+  *tail_bytes = 0;
+  for (int o = 0; o < nobjects; o++) {
+    int64_t ns = 0, nf = 0, cl = 0;
+    int rc = nxec_object_layout(n, k, lengths[o], max_chunk_size, &ns, &nf, &cl);
+    if (rc) return rc;
+    *total_stripes += ns;
+    if (ns > nf) *tail_bytes += (int64_t(k) * cl + 15) / 16 * 16;
+  }
+  return NXEC_OK;
+}
+
+int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
+                        const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
+                        unsigned char *d_tail, unsigned char *d_md5, void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  int64_t total = 0, tail_total = 0;
+  int rc = nxec_objects_layout(n, k, nobjects, lengths, max_chunk_size, &total, &tail_total);
+  if (rc) return rc;
+  if (total == 0) return NXEC_OK;
+  const int p = n - k;
+  const int64_t M = max_chunk_size;
+  if (!d_objects || (p > 0 && !d_parity) || (tail_total > 0 && !d_tail))
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_objects: null buffer");
+  for (int o = 0; o < nobjects; o++)
+    if (lengths[o] > 0 && !d_objects[o]) return set_error(NXEC_ERR_INVALID, "nxec_encode_objects: object %d is NULL", o);
+  rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);
+  const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
+
+  // host plan: full stripes of every object as gather pointer tables (one fast
+  // launch), last stripes as padded copies + a variable-length list launch,
+  // every chunk an MD5 item; all tables go to the device in one copy
+  std::vector<const uint8_t *> fsrc;
+  std::vector<uint8_t *> fdst;
+  std::vector<PadCopy> pads;
+  std::vector<ListStripe> tails;
+  std::vector<int64_t> prefix(1, 0);
+  std::vector<Md5Item> items;
+  bool full_aligned = M % 16 == 0;
+  int64_t g = 0, toff = 0;
+  for (int o = 0; o < nobjects; o++) {
+    int64_t ns = 0, nf = 0, cl = 0;
+    nxec_object_layout(n, k, lengths[o], M, &ns, &nf, &cl);
+    const uint8_t *obj = d_objects[o];
+    full_aligned &= (reinterpret_cast<uintptr_t>(obj) & 15) == 0 || nf == 0;
+    for (int64_t s = 0; s < ns; s++, g++) {
+      uint8_t *par = d_parity ? d_parity + g * p * M : nullptr;
+      uint8_t *dig = d_md5 ? d_md5 + g * n * 16 : nullptr;
+      if (s < nf) {
+        for (int j = 0; j < k; j++) fsrc.push_back(obj + (s * k + j) * M);
+        for (int i = 0; i < p; i++) fdst.push_back(par + i * M);
+        if (dig) {
+          for (int j = 0; j < k; j++) items.push_back({obj + (s * k + j) * M, M, dig + j * 16});
+          for (int i = 0; i < p; i++) items.push_back({par + i * M, M, dig + (k + i) * 16});
+        }
+      } else {  // last stripe: zero-padded copy to the tail arena (chunk_manager.cc:390-399)
+        uint8_t *td = d_tail + toff;
+        const int64_t rem = lengths[o] - nf * k * M;
+        pads.push_back({obj + nf * k * M, td, rem, int64_t(k) * cl});
+        tails.push_back({td, par, cl, cl, M});
+        prefix.push_back(prefix.back() + (cl + 15) / 16);
+        if (dig) {
+          for (int j = 0; j < k; j++) items.push_back({td + j * cl, cl, dig + j * 16});
+          for (int i = 0; i < p; i++) items.push_back({par + i * M, cl, dig + (k + i) * 16});
+        }
+        toff += (int64_t(k) * cl + 15) / 16 * 16;
+      }
+    }
+  }
+  const int64_t nfs = static_cast<int64_t>(fsrc.size()) / k;
+  // full stripes of unaligned objects go through the list kernel instead
+  if (!full_aligned && nfs > 0) {
+    for (int64_t f = 0; f < nfs; f++) {
+      tails.push_back({fsrc[f * k], p > 0 ? fdst[f * p] : nullptr, M, M, M});
+      prefix.push_back(prefix.back() + (M + 15) / 16);
+    }
+  }
+  const size_t b_fsrc = fsrc.size() * sizeof(void *), b_fdst = fdst.size() * sizeof(void *);
+  const size_t b_pads = pads.size() * sizeof(PadCopy), b_tails = tails.size() * sizeof(ListStripe);
+  const size_t b_pref = prefix.size() * sizeof(int64_t), b_items = items.size() * sizeof(Md5Item);
+  size_t off[7] = {0};
+  const size_t sizes[6] = {b_fsrc, b_fdst, b_pads, b_tails, b_pref, b_items};
+  for (int i = 0; i < 6; i++) off[i + 1] = off[i] + (sizes[i] + 15) / 16 * 16;
+  Slot *slot = nullptr;
+  rc = acquire_slot(ctx, std::max<size_t>(off[6], 16), &slot);
+  if (rc) return rc;
+  const void *srcs[6] = {fsrc.data(), fdst.data(), pads.data(), tails.data(), prefix.data(), items.data()};
+  // the slot's staging may still be in use by an earlier call on its own stream
+  rc = hip_check(hipStreamSynchronize(slot->stream), "slot sync");
+  for (int i = 0; i < 6 && !rc; i++)
+    if (sizes[i]) std::memcpy(slot->h + off[i], srcs[i], sizes[i]);
+  if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[6], hipMemcpyHostToDevice, st), "tables H2D");
+  auto dptr = [&](int i) { return slot->d + off[i]; };
+  if (!rc && p > 0 && full_aligned && nfs > 0)
+    rc = stripes_mul_impl(ctx, p, k, prow, nullptr, reinterpret_cast<const unsigned char *const *>(dptr(0)), nullptr,
+                          0, 0, nullptr, reinterpret_cast<unsigned char *const *>(dptr(1)), nullptr, 0, 0, nullptr, M,
+                          nfs, st);
+  if (!rc) rc = launch_pad_copy(reinterpret_cast<const PadCopy *>(dptr(2)), int64_t(pads.size()), st);
+  if (!rc && p > 0)
+    rc = launch_mul_list(p, k, prow, reinterpret_cast<const ListStripe *>(dptr(3)),
+                         reinterpret_cast<const int64_t *>(dptr(4)), int64_t(tails.size()), prefix.back(),
+                         ctx->num_cus, st);
+  if (!rc && !items.empty()) rc = launch_md5_list(reinterpret_cast<const Md5Item *>(dptr(5)), int64_t(items.size()), st);
+  // the tables live in the slot: drain before handing it back (synchronous call)
+  const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
+  release_slot(ctx, slot);
+  return rc ? rc : rc2;
+}
+
 int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream) {

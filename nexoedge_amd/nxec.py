@@ -98,6 +98,15 @@ def object_layout(n: int, k: int, length: int, max_chunk_size: int):
     return ns.value, nf.value, cl.value
 
 
+def objects_layout(n: int, k: int, lengths: Sequence[int], max_chunk_size: int):
+    """(total_stripes, tail_bytes) of a multi-object batch (nxec_objects_layout)."""
+    ln = np.ascontiguousarray(np.asarray(list(lengths), dtype=np.int64))
+    ts, tb = C.c_int64(), C.c_int64()
+    check(lib.nxec_objects_layout(n, k, len(ln), C.c_void_p(ln.ctypes.data), max_chunk_size, C.byref(ts),
+                                  C.byref(tb)), "nxec_objects_layout")
+    return ts.value, tb.value
+
+
 def car_plan(n: int, k: int, failed: int, groups: Sequence[Sequence[int]]):
     """CAR repair plan (chunk_manager.cc:929-986) -> list of (chunk_ids, coeffs) per agent sub-group."""
     keep, op, cp = _groups(groups)
@@ -325,6 +334,14 @@ class Context:
         check(lib.nxec_encode_object(C.c_void_p(self.ptr), n, k, C.c_void_p(int(obj)), length, max_chunk_size,
                                      C.c_void_p(int(parity)), C.c_void_p(int(tail) if tail else None),
                                      C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_object")
+
+    def encode_objects(self, n: int, k: int, objects: Sequence[int], lengths: Sequence[int], max_chunk_size: int,
+                       parity: int, tail=None, md5=None, stream=None) -> None:
+        ptrs = (C.c_void_p * max(len(objects), 1))(*[int(o) if o else None for o in objects])
+        ln = np.ascontiguousarray(np.asarray(list(lengths), dtype=np.int64))
+        check(lib.nxec_encode_objects(C.c_void_p(self.ptr), n, k, len(ln), ptrs, C.c_void_p(ln.ctypes.data),
+                                      max_chunk_size, C.c_void_p(int(parity)), C.c_void_p(int(tail) if tail else None),
+                                      C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_objects")
 
     def encode_object_host(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int,
                            md5=None, batch_stripes: int = 0) -> None:

@@ -544,3 +544,48 @@ def test_survey_named_encode_entry_points(gpu_ctx):
         assert all(np.array_equal(got[s, r], w[r]) for r in range(rows))
     db.free()
     pb.free()
+
+
+@pytest.mark.parametrize("misalign", [0, 3])
+def test_encode_objects_matches_per_object(gpu_ctx, misalign):
+    """Many objects per call (full stripes in one gather launch, last stripes in
+    one variable-length launch, MD5 of every chunk in one list launch) equals
+    encoding each object on its own with nxec_encode_object."""
+    n, k, M = 9, 6, 4096
+    p = n - k
+    lengths = [0, 1, 17, k * M - 1, k * M, 3 * k * M + 100, 5000, 2 * k * M, 12345]
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    assert total == sum(nxec.object_layout(n, k, L, M)[0] for L in lengths)
+    offs, pos = [], 0
+    for L in lengths:
+        offs.append(pos + misalign)
+        pos += (L + misalign + 15) // 16 * 16 + 16
+    host = np.zeros(pos + 16, dtype=np.uint8)
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        host[o:o + L] = fill_bytes(L, 100 + i)
+    arena = up(host)
+    par = nxec.DeviceBuffer(max(total * p * M, 1))
+    tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+    md5 = nxec.DeviceBuffer(total * n * 16)
+    gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
+    gp = par.download().reshape(total, p, M)
+    gm = md5.download().reshape(total, n, 16)
+    g = 0
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        if ns == 0:
+            continue
+        ob = up(host[o:o + L])
+        op, ot, om = nxec.DeviceBuffer(ns * p * M), nxec.DeviceBuffer(k * M), nxec.DeviceBuffer(ns * n * 16)
+        gpu_ctx.encode_object(n, k, ob.ptr, L, M, op.ptr, ot.ptr, om.ptr)
+        gpu_ctx.sync()
+        wp = op.download().reshape(ns, p, M)
+        for s in range(ns):
+            cs = M if s < nf else cl
+            assert np.array_equal(gp[g + s, :, :cs], wp[s, :, :cs]), (i, s)
+        assert np.array_equal(gm[g:g + ns], om.download().reshape(ns, n, 16)), i
+        g += ns
+        for b in (ob, op, ot, om):
+            b.free()
+    for b in (arena, par, tail, md5):
+        b.free()
