@@ -5,7 +5,8 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 CXXSTD   := -std=c++17
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC $(CXXSTD) -Wall -Iinclude -Inexoedge_amd/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC $(CXXSTD) -Wall -Iinclude -Inexoedge_amd/csrc \
+            -mllvm -amdgpu-atomic-optimizer-strategy=None
 LIBDIR   := nexoedge_amd/lib
 CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
@@ -39,10 +40,12 @@ oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_ora
 	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c oracle/nxec_cpu_simd.c -o $@ -lpthread
 
 # design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
-tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling
+tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling tools/microbench/mem_pattern
 tools/microbench/shape_ceiling: tools/microbench/shape_ceiling.hip $(LIBDIR)/libnxec.so
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 tools/microbench/tune_mul: tools/microbench/tune_mul.hip $(LIBDIR)/libnxec.so
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
+tools/microbench/mem_pattern: tools/microbench/mem_pattern.hip $(LIBDIR)/libnxec.so
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 tools/microbench/lut_variants: tools/microbench/lut_variants.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@

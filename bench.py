@@ -195,7 +195,7 @@ def wl_rs10_4(args, ctx, stream, rank):
         "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
     }
     return Workload("rs10_4", "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident", config, ops, [buf],
-                    f"k_mul_vec<K={k},R=16> (encode launch)", ns)
+                    f"k_mul_vec<K={k},R=8> work-queue (encode launch)", ns)
 
 
 def wl_repair12(args, ctx, stream, rank):
@@ -268,7 +268,7 @@ def wl_write14(args, ctx, stream, rank):
                           f"{ns} stripes per GPU", "stripes_per_gpu": ns, "chunk_bytes": cs,
               "byte_accounting": "encode n*cs + md5 n*cs per stripe"}
     return Workload("write14", "GiB/s RS(10,4) encode + per-chunk MD5, 1 MiB chunks, device-resident", config, ops,
-                    [buf, dig], f"k_mul_vec<K={k},R=16> (encode launch)", ns)
+                    [buf, dig], f"k_mul_vec<K={k},R=8> work-queue (encode launch)", ns)
 
 
 def wl_object(args, ctx, stream, rank):

@@ -16,6 +16,7 @@ int repair_rows(int n, int k, const std::vector<uint8_t> &enc, const int32_t *in
                 int ntargets, uint8_t *out);
 
 constexpr int kMaxRowsPerPass = 4;  // one packed 32-bit LDS entry holds 4 row products
+constexpr int kQueueSlots = 4096;   // per-launch tile-queue slots (device ring, see nxec_kernels.hip)
 constexpr uint32_t kNoCopy = 0xFFFFFFFFu;
 
 // Kernel arguments of one GF(2^8) stripe-multiply pass (<= 4 output rows).
@@ -37,6 +38,8 @@ struct MulArgs {
   int32_t any_copy;                 // copy_idx has entries >= 0
   int32_t dst_ptr_row0;             // gather mode: first row of this pass inside dst_ptrs[s*rows_total + r]
   int32_t dst_ptr_rows;             // gather mode: rows_total
+  int32_t queue_slot;               // tile-queue slot of this launch (set by launch_mul)
+  uint32_t tiles_per_grab;          // work-queue run length (set by launch_mul)
   // strided form: byte offsets of the chunks inside a stripe (idx * chunk_stride,
   // precomputed on the host; < 4 GiB so they stay single 32-bit SGPRs)
   uint32_t src_off[NXEC_MAX_K + 1];

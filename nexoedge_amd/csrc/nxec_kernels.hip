@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <utility>
@@ -50,6 +51,9 @@ constexpr int kPermPrefetchMaxK = 4;
 constexpr int kPermMaxK = 13;  // beyond this the single-row VALU kernel would spill (128-VGPR budget)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRingBytes = 16;  // work-queue broadcast ring, after the tables in dynamic LDS
+constexpr bool queue_fits(int table_bytes) { return table_bytes + kRingBytes <= kLdsBytes; }
 
 // Streaming (nontemporal) 16-byte accesses: every source byte is read once and
 // every parity byte written once, so keep them from displacing the tables'
@@ -243,30 +247,147 @@ struct PermBody {
   }
 };
 
-// Persistent tile loop.  Workgroup b owns the contiguous tile run
-// [b*ntiles/G, (b+1)*ntiles/G): consecutive 16 KiB column tiles of the same
-// stripes, so each CU walks its own few stripes sequentially (page / DRAM-row
-// locality; +4% over interleaving tiles across workgroups at RS(10,4) 1 MiB,
-// tools/microbench/tune_mul.hip PF4 vs PF3).  With PF the next tile's loads
-// go out before this tile's compute through two ping-pong register buffers
-// (manual 2x unroll pinned by sched_barrier: no register copies, so the
-// waitcnt pass keeps the prefetch in flight); the final prefetch re-reads the
-// current tile instead of branching, so every path has the same loads in flight.
-template <int K, bool GATHER, bool FULL, bool PF, class Body>
-__device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body) {
+// Per-launch tile queues (one 128-byte slot per launch: [0] next tile, [1]
+// workgroups finished).  The last workgroup to finish resets its slot, so a
+// slot is clean for the next launch that draws it (host ring, kQueueSlots).
+__device__ uint32_t g_tile_queue[kQueueSlots * 32];
+
+// Work-queue grab: global_atomic_add with return, issued through inline asm
+// so the compiler's wait-count bookkeeping never sees it.  Issued before a
+// step's K loads, it is older than every op the compiler waits for, so the
+// compiler's own waits stay correct (they can only wait longer), and the
+// caller publishes g after an explicit vmcnt(K) -- instead of the vmcnt(0)
+// (drain of every store) the compiler emits around a divergent atomic.
+__device__ __forceinline__ uint32_t grab_async(uint32_t *q) {
+  uint32_t g;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(g) : "v"(q), "v"(1u) : "memory");
+  return g;
+}
+// ring[OFF/4] = g once at most N vector-memory ops are outstanding
+template <int N, int OFF>
+__device__ __forceinline__ void publish(uint32_t ring_base, uint32_t g) {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%2)\n\tds_write_b32 %0, %1 offset:%3" ::"v"(ring_base), "v"(g), "n"(N), "n"(OFF)
+               : "memory");
+}
+
+// Persistent tile loop.
+//
+// Q (work queue, the default where 16 bytes of LDS are free): workgroups pull
+// runs of T consecutive 16 KiB column tiles from a per-launch atomic counter
+// (T = 1 for wide stripes; more for narrow ones so the counter is not
+// hammered, tiles_per_grab()), the next run grabbed one run ahead and
+// broadcast through a 4-entry LDS ring (one barrier per run).  In-flight tiles therefore always form one compact,
+// ascending address window, and a workgroup slowed by a busy HBM channel
+// simply takes fewer tiles: +12 % over static tile runs for the same bytes
+// (tools/microbench/mem_pattern.hip, profiles/r01_mem_pattern.log).
+//
+// !Q (tables fill the whole 160 KiB), or queue_slot < 0 (NXEC_TILE_ORDER=static,
+// for A/B only): workgroup b owns the contiguous tile run [b*ntiles/G, (b+1)*ntiles/G).
+//
+// PF: the next tile's loads go out before this tile's compute through two
+// ping-pong register buffers (manual 2x unroll pinned by sched_barrier: no
+// register copies, so the waitcnt pass keeps the prefetch in flight); a final
+// prefetch past the end re-reads the current tile instead of branching, so
+// every path has the same loads in flight.
+template <int K, bool GATHER, bool FULL, bool PF, bool Q, class Body>
+__device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, uint32_t *ring) {
   const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
   const uint32_t tps = (nvec + kBlock - 1) / kBlock;
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  auto run = [&](uint32_t tt, const u32x4(&d)[K]) {
+    const TilePos p = tile_pos(tt, tps);
+    if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
+  };
+  if (Q && a.queue_slot >= 0) {
+    uint32_t *q = g_tile_queue + static_cast<size_t>(a.queue_slot) * 32;
+    const uint32_t T = a.tiles_per_grab;  // a grab = a run of T consecutive tiles
+    if (threadIdx.x == 0) {
+      ring[2] = atomicAdd(q, 1u);
+      ring[3] = atomicAdd(q, 1u);
+    }
+    __syncthreads();
+    // t: current tile; [t, rend) the rest of its run; nrun: first tile of the
+    // run already grabbed for after it (all wave-uniform, SGPRs)
+    uint32_t t = __builtin_amdgcn_readfirstlane(ring[2]) * T;
+    uint32_t nrun = __builtin_amdgcn_readfirstlane(ring[3]) * T;
+    uint32_t rend = t + T < ntiles ? t + T : ntiles;
+    int slot = 0;
+    // LDS byte address of ring[0], materialized once (a VGPR that no store
+    // ever uses, so publishing never waits on the stores in flight)
+    uint32_t ring_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ring));
+    asm volatile("" : "+v"(ring_base));
+    // barrier that orders only the LDS ring (global loads stay in flight)
+    auto ring_barrier = [] {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
+    // one tile: at the last tile of a run, grab the run after next (thread 0,
+    // early, so the atomic's latency hides behind this tile's work) and
+    // broadcast it at the end; nxt (PF) receives the next tile's sources
+    // (the grab is issued before this step's loads: the ring write then only
+    // waits for the atomic, not for the loads and stores behind it)
+    auto step = [&](u32x4(&cur)[K], u32x4(&nxt)[K], bool pf) {
+      const bool edge = t + 1 >= rend;
+      const uint32_t tn = edge ? nrun : t + 1;
+      uint32_t g = 0;
+      if (edge && threadIdx.x == 0) g = grab_async(q);
+      if (pf) {
+        load_tile<K, GATHER, FULL>(a, tile_pos(tn < ntiles ? tn : t, tps), nvec, nxt);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, cur);
+        __builtin_amdgcn_sched_barrier(0);  // all K loads in flight before the lookups
+      }
+      run(t, cur);
+      if (edge) {
+        if (threadIdx.x == 0) {
+          // >= K vector-memory ops (this step's loads) were issued after the
+          // grab, so at most K outstanding means the grab has returned
+          if (slot == 0) publish<FULL ? K : 0, 0>(ring_base, g);
+          else publish<FULL ? K : 0, 4>(ring_base, g);
+        }
+        ring_barrier();
+        const uint32_t nn = __builtin_amdgcn_readfirstlane(ring[slot]) * T;
+        slot ^= 1;
+        rend = nrun + T < ntiles ? nrun + T : ntiles;
+        nrun = nn;
+      }
+      t = tn;
+      return t < ntiles;
+    };
+    if (t < ntiles) {
+      if constexpr (PF) {
+        u32x4 A[K], B[K];
+        load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
+        while (step(A, B, true) && step(B, A, true)) {
+        }
+      } else {
+        bool more = true;
+        while (more) {
+          u32x4 d[K];
+          more = step(d, d, false);
+        }
+      }
+    }
+    // every grab of this workgroup has returned (its values were consumed);
+    // the last workgroup out resets the slot for the next launch
+    if (threadIdx.x == 0) {
+      __threadfence();
+      if (atomicAdd(q + 1, 1u) == gridDim.x - 1) {
+        atomicExch(q, 0u);
+        atomicExch(q + 1, 0u);
+      }
+    }
+    return;
+  }
   // readfirstlane: the tile index is wave-uniform; keep its math on the SALU
   uint32_t t = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x) * ntiles) / gridDim.x));
   const uint32_t tend = __builtin_amdgcn_readfirstlane(
       static_cast<uint32_t>((static_cast<uint64_t>(blockIdx.x + 1) * ntiles) / gridDim.x));
   if (t >= tend) return;
-  auto run = [&](uint32_t tt, const u32x4(&d)[K]) {
-    const TilePos p = tile_pos(tt, tps);
-    if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
-  };
   if constexpr (PF) {
     u32x4 A[K], B[K];
     load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
@@ -296,14 +417,17 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body) {
 // Fully unrolled vector kernels: all K source loads of a column vector in
 // flight.  COPY: fused pass-through of sources (full-output decode); a
 // separate instantiation so encode/recover kernels carry no copy registers.
+// The queue ring lives in the dynamic LDS block after the tables (Q only
+// where it fits: queue_fits()).
 template <int K, int R, bool GATHER, bool COPY, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
   constexpr bool PF = K <= ((COPY || !FULL) ? kPrefetchMaxKCopy : kPrefetchMaxK);
+  constexpr bool Q = queue_fits(LdsBody<K, R, GATHER, COPY>::kLds);
   using Body = LdsBody<K, R, GATHER, COPY>;
   extern __shared__ uint32_t tab[];
   Body::setup(a, tab);
   __syncthreads();
-  tile_loop<K, GATHER, FULL, PF>(a, Body(tab));
+  tile_loop<K, GATHER, FULL, PF, Q>(a, Body(tab), tab + Body::kLds / 4);
 }
 
 template <int K, bool GATHER, bool COPY, bool FULL>
@@ -313,7 +437,7 @@ __global__ __launch_bounds__(kBlock) void k_mul_perm(const MulArgs a) {
   extern __shared__ uint32_t tab[];
   Body::setup(a, tab);
   __syncthreads();
-  tile_loop<K, GATHER, FULL, PF>(a, Body(tab));
+  tile_loop<K, GATHER, FULL, PF, true>(a, Body(tab), tab + Body::kLds / 4);
 }
 
 // Runtime-k vector kernel (k > kMaxTemplK), R = 1 tables, sources in groups of 4.
@@ -558,7 +682,11 @@ int choose_r(int k, bool tunable) {
   const int want = env ? std::atoi(env) : 0;
   if (want == 1) return 1;
   if (want == 8) return 8;
-  return k <= 10 ? 16 : 8;
+  if (want == 16 && k <= 10) return 16;
+  // the largest replication that leaves room for the tile-queue ring: the
+  // queue's dynamic tile order is worth far more than R = 16's fewer LDS bank
+  // conflicts (k = 10: 0.80 vs 0.64-0.73 of 8 TB/s, profiles/r01_mem_pattern.log)
+  return k <= 9 ? 16 : 8;
 }
 
 KernelFn vec_kernel(int k, int r, bool gather, bool copy, bool full) {
@@ -568,7 +696,12 @@ KernelFn vec_kernel(int k, int r, bool gather, bool copy, bool full) {
   return kDefR8[gather][copy][full][k - 1];
 }
 
-int default_r(int k) { return choose_r(k, false); }
+
+// dynamic LDS of a k_mul_vec instantiation: tables (+ the queue ring where it fits)
+int table_lds(int k, int r) {
+  const int t = k * 1024 * r;
+  return queue_fits(t) ? t + kRingBytes : t;
+}
 
 }  // namespace
 
@@ -589,14 +722,19 @@ LaunchInfo plan_launch(int k, int rows, int64_t vec_count, int64_t nstripes, int
   if (use_perm(k, rows, full, copy, gather)) {
     li.perm = true;
     li.lds_copies = 0;
-    li.lds_bytes = k * 32;
+    li.lds_bytes = k * 32 + kRingBytes;
     li.variant = "vec_perm";
   } else {
     li.lds_copies = choose_r(k, tunable);
     li.lds_bytes = k * 1024 * li.lds_copies;
+    const bool queued = k <= kMaxTemplK && queue_fits(li.lds_bytes);
+    if (queued) li.lds_bytes += kRingBytes;
     per_cu = kLdsBytes / (li.lds_bytes > 0 ? li.lds_bytes : 1);
     if (per_cu > 2) per_cu = 2;  // 2 x 16 waves = the CU's 32-wave limit
     if (per_cu < 1) per_cu = 1;
+    // queue-driven launches: one workgroup per CU keeps the in-flight window
+    // tightest (two per CU measured 0.755 vs 0.798 of 8 TB/s, XOR probe)
+    if (queued) per_cu = 1;
     li.variant = k > kMaxTemplK ? "vec_dyn" : "vec_lds";
   }
   const int64_t tps = (vec_count + kBlock - 1) / kBlock;
@@ -616,12 +754,14 @@ int prepare_kernels() {
       for (int c = 0; c < 2; c++)
         for (int f = 0; f < 2; f++) {
           if (g && c) continue;
-          const int r = default_r(k);
-          hipError_t e = raise(vec_kernel(k, r, g, c, f), k * 1024 * r);
-          if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec)");
+          for (int r : {16, 8}) {
+            if (r == 16 && k > 10) continue;
+            hipError_t e = raise(vec_kernel(k, r, g, c, f), table_lds(k, r));
+            if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec)");
+          }
         }
-    hipError_t e = raise(kTuneR1[k - 1], k * 1024);
-    if (e == hipSuccess) e = raise(kDefR8[0][0][1][k - 1], k * 1024 * 8);
+    hipError_t e = raise(kTuneR1[k - 1], table_lds(k, 1));
+    if (e == hipSuccess) e = raise(kDefR8[0][0][1][k - 1], table_lds(k, 8));
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(k_mul_vec tune)");
   }
   for (KernelFn fn : {&k_mul_vec_dyn<false>, &k_mul_vec_dyn<true>, &k_mul_bytes<false>, &k_mul_bytes<true>}) {
@@ -629,6 +769,29 @@ int prepare_kernels() {
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(dyn/bytes)");
   }
   return NXEC_OK;
+}
+
+// Work-queue run length: about 12 tiles' worth of chunk traffic per grab (a
+// 16 KiB tile moves k + rows (+ copies) 16 KiB pieces), so wide stripes grab
+// one tile at a time (the tightest in-flight window) and narrow ones (CAR XOR,
+// small partial encodes) several, which keeps the single counter well under
+// its atomic rate (~80 M/s) and the grab latency hidden.
+uint32_t tiles_per_grab(const MulArgs &a) {
+  int units = a.k + a.rows;
+  if (a.any_copy)
+    for (int j = 0; j < a.k; j++) units += a.copy_off[j] != kNoCopy;
+  const int t = (12 + units - 1) / units;
+  return static_cast<uint32_t>(t < 1 ? 1 : (t > 8 ? 8 : t));
+}
+
+// host side of the tile-queue ring: each vector launch draws the next slot
+// (4096 launches would have to be in flight at once for two to share one)
+std::atomic<uint32_t> g_next_slot{0};
+
+// NXEC_TILE_ORDER=static: static tile runs instead of the work queue (A/B probes only)
+bool static_order() {
+  const char *env = std::getenv("NXEC_TILE_ORDER");
+  return env && std::strcmp(env, "static") == 0;
 }
 
 int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
@@ -646,6 +809,8 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
     for (int pi = 0; pi < 2; pi++) {
       if (parts[pi][1] <= 0) continue;
       MulArgs b = a;
+      b.queue_slot = static_order() ? -1 : static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
+      b.tiles_per_grab = tiles_per_grab(b);
       b.vec_begin = a.vec_begin + parts[pi][0];
       b.vec_count = parts[pi][1];
       const bool is_full = pi == 0;

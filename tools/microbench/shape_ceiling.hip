@@ -202,9 +202,11 @@ void run_shape(int ncu, long S, int reps, nxec_ctx_t *ctx) {
   } ms[] = {{"xor(ceiling)", k_shape<K, ROWS, 0, 1>, 0, nullptr},
             {"lds", k_shape<K, ROWS, 1, R>, K * 1024 * R, dpk},
             {"perm", k_shape<K, ROWS, 2, 1>, ROWS * K * 32, dnb},
-            {"PRODUCT", nullptr, 0, nullptr}};
+            {"PRODUCT", nullptr, 0, nullptr},
+            {"PRODUCT-static", nullptr, 0, nullptr}};
   unsigned long long ref = 0;
-  for (int mi = 0; mi < 4; mi++) {
+  for (int mi = 0; mi < 5; mi++) {
+    if (mi == 4) setenv("NXEC_TILE_ORDER", "static", 1);
     Args a{buf, ms[mi].tab, cs, S};
     auto go = [&]() {
       if (ms[mi].fn) {
@@ -240,6 +242,7 @@ void run_shape(int ncu, long S, int reps, nxec_ctx_t *ctx) {
     printf("k=%2d rows=%d %-13s %7.3f ms  %7.1f GB/s  frac8T %.3f  %s\n", K, ROWS, ms[mi].name, tot / reps,
            bytes / (tot / reps * 1e-3) / 1e9, bytes / (tot / reps * 1e-3) / 8e12,
            mi == 0 ? "" : (h == ref ? "MATCH" : "MISMATCH"));
+    unsetenv("NXEC_TILE_ORDER");
   }
   CHECK(hipFree(buf));
   CHECK(hipFree(dpk));
