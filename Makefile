@@ -40,12 +40,14 @@ oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_ora
 	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c oracle/nxec_cpu_simd.c -o $@ -lpthread
 
 # design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
-tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling tools/microbench/mem_pattern
+tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling tools/microbench/mem_pattern tools/microbench/chunk_stride
 tools/microbench/shape_ceiling: tools/microbench/shape_ceiling.hip $(LIBDIR)/libnxec.so
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 tools/microbench/tune_mul: tools/microbench/tune_mul.hip $(LIBDIR)/libnxec.so
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 tools/microbench/mem_pattern: tools/microbench/mem_pattern.hip $(LIBDIR)/libnxec.so
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
+tools/microbench/chunk_stride: tools/microbench/chunk_stride.hip $(LIBDIR)/libnxec.so
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -Iinclude $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)' -o $@
 tools/microbench/lut_variants: tools/microbench/lut_variants.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@

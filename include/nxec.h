@@ -252,10 +252,13 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
  * pointers, lengths[o] bytes) is split as in nxec_object_layout; its stripes
  * follow the previous objects' in one global stripe order g.  Parity chunk
  * (g, i) at d_parity + (g*(n-k) + i)*M; digests (NULL = skip) at
- * d_md5 + g*n*16; the zero-padded data chunks of each object's last stripe
- * are written to the d_tail arena (size from nxec_objects_layout).  Full
- * stripes of all objects run as one gather launch, last stripes as one
- * variable-length launch, every chunk's MD5 as one launch.  Synchronous
+ * d_md5 + g*n*16.  The data chunks of each object's last stripe (chunk size
+ * cl) are written zero-padded to the d_tail arena (size from
+ * nxec_objects_layout), objects in order, chunk j of an object at
+ * tail_off + j*cls with cls = cl rounded up to 16 (bytes [cl, cls) zero;
+ * the object's tail_off advances by k*cls).  Full stripes of all objects run
+ * as one gather launch, last stripes as one work-queue launch over
+ * variable-length stripes, every chunk's MD5 as one launch.  Synchronous
  * (returns when the work is done). */
 int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int64_t max_chunk_size,
                         int64_t *total_stripes, int64_t *tail_bytes);

@@ -92,6 +92,25 @@ struct ListStripe {
 // rows x k coefficients (rows <= 4 per pass inside); d_stripes / d_prefix in device memory
 int launch_mul_list(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const int64_t *d_prefix,
                     int64_t nstripes, int64_t total_units, int num_cus, void *stream);
+// Ragged stripes (aligned: src, dst, src_cs, dst_cs, len all multiples of 16)
+// through the work-queue LDS-table kernel; tile t is column tile
+// t - stripe_tile0[s] of stripe s = tile_stripe[t] (1024 16-byte vectors each).
+constexpr int kMaxRaggedK = 19;
+int launch_mul_ragged(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const uint32_t *d_tile_stripe,
+                      const uint32_t *d_stripe_tile0, int64_t ntiles, int num_cus, void *stream);
+// Last stripe of an object into the aligned tail arena: dst + j*cls (j < k)
+// receives object bytes [j*cl, (j+1)*cl) of src (zeros past rem) then zeros
+// up to cls (a multiple of 16 >= cl).  Item i owns 256-thread blocks
+// [bstart[i], bstart[i+1]) of kPadVecs*256 16-byte vectors (cls/16*k in all).
+constexpr int kPadVecs = 8;
+struct PadChunks {
+  const uint8_t *src;
+  uint8_t *dst;
+  int64_t rem, cl, cls;
+  int64_t k;
+};
+int launch_pad_chunks(const PadChunks *d_items, const uint32_t *d_bstart, int64_t nitems, int64_t nblocks,
+                      void *stream);
 // copy item i: dst[0 .. dst_len) = src[0 .. src_len) then zeros (src_len <= dst_len)
 struct PadCopy {
   const uint8_t *src;

@@ -76,17 +76,21 @@ __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
   return p;
 }
 
-// entry x of source j: byte r = c(r, j) * x
+// entry x of source j: byte r = c(r, j) * x (coef row-major rows x k)
 template <int R>
-__device__ __forceinline__ void build_tables(const MulArgs &a, int k, uint32_t *tab) {
+__device__ __forceinline__ void build_tables(const uint8_t *coef, int k, int rows, uint32_t *tab) {
   for (int i = threadIdx.x; i < k * 256; i += blockDim.x) {
     const int j = i >> 8;
     const uint32_t x = static_cast<uint32_t>(i & 255);
     uint32_t e = 0;
-    for (int r = 0; r < a.rows; r++) e |= gf_mul_dev(a.coef[r * a.k + j], x) << (8 * r);
+    for (int r = 0; r < rows; r++) e |= gf_mul_dev(coef[r * k + j], x) << (8 * r);
 #pragma unroll
     for (int c = 0; c < R; c++) tab[i * R + c] = e;
   }
+}
+template <int R>
+__device__ __forceinline__ void build_tables(const MulArgs &a, int k, uint32_t *tab) {
+  build_tables<R>(a.coef, a.k, a.rows, tab);
 }
 
 // Chunk addresses of stripe s.  GATHER is a template parameter so the
@@ -124,6 +128,27 @@ __device__ __forceinline__ void store_rows(const MulArgs &a, uint32_t s, uint32_
   for (int r = 0; r < kMaxRowsPerPass; r++) {
     if (r < a.rows) st_stream(dst_row<GATHER>(a, s, r) + static_cast<size_t>(v) * 16, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
   }
+}
+
+// the same transpose, row r (< rows) stored at row0 + r*row_stride + v*16
+__device__ __forceinline__ void store_rows_ptr(uint8_t *row0, int64_t row_stride, int rows, uint32_t v,
+                                               const uint32_t acc[16]) {
+  uint32_t o[4][4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
+    const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);
+    const uint32_t hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
+    const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
+    const uint32_t hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+    o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
+    o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
+    o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
+    o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
+  }
+#pragma unroll
+  for (int r = 0; r < kMaxRowsPerPass; r++)
+    if (r < rows) st_stream(row0 + r * row_stride + static_cast<size_t>(v) * 16, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
 }
 
 template <int R>
@@ -290,18 +315,15 @@ __device__ __forceinline__ void publish(uint32_t ring_base, uint32_t g) {
 // register copies, so the waitcnt pass keeps the prefetch in flight); a final
 // prefetch past the end re-reads the current tile instead of branching, so
 // every path has the same loads in flight.
-template <int K, bool GATHER, bool FULL, bool PF, bool Q, class Body>
-__device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, uint32_t *ring) {
-  const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
-  const uint32_t tps = (nvec + kBlock - 1) / kBlock;
-  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  auto run = [&](uint32_t tt, const u32x4(&d)[K]) {
-    const TilePos p = tile_pos(tt, tps);
-    if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
-  };
-  if (Q && a.queue_slot >= 0) {
-    uint32_t *q = g_tile_queue + static_cast<size_t>(a.queue_slot) * 32;
-    const uint32_t T = a.tiles_per_grab;  // a grab = a run of T consecutive tiles
+//
+// The geometry is the caller's: load(t, d) fetches tile t's K source vectors
+// of this lane into d, run(t, d) computes and stores tile t.  ntiles tiles;
+// slot >= 0 selects the queue (Q kernels), T = tiles per grab.
+template <int K, bool PF, bool Q, bool QWAIT_K, class LoadF, class RunF>
+__device__ __forceinline__ void tile_loop(const LoadF &load, const RunF &run, uint32_t ntiles, int32_t slot_arg,
+                                          uint32_t T, uint32_t *ring) {
+  if (Q && slot_arg >= 0) {
+    uint32_t *q = g_tile_queue + static_cast<size_t>(slot_arg) * 32;
     if (threadIdx.x == 0) {
       ring[2] = atomicAdd(q, 1u);
       ring[3] = atomicAdd(q, 1u);
@@ -309,8 +331,9 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
     __syncthreads();
     // t: current tile; [t, rend) the rest of its run; nrun: first tile of the
     // run already grabbed for after it (all wave-uniform, SGPRs)
-    uint32_t t = __builtin_amdgcn_readfirstlane(ring[2]) * T;
-    uint32_t nrun = __builtin_amdgcn_readfirstlane(ring[3]) * T;
+    auto run_start = [&](uint32_t r) -> uint32_t { return r * T; };
+    uint32_t t = run_start(__builtin_amdgcn_readfirstlane(ring[2]));
+    uint32_t nrun = run_start(__builtin_amdgcn_readfirstlane(ring[3]));
     uint32_t rend = t + T < ntiles ? t + T : ntiles;
     int slot = 0;
     // LDS byte address of ring[0], materialized once (a VGPR that no store
@@ -334,10 +357,10 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
       uint32_t g = 0;
       if (edge && threadIdx.x == 0) g = grab_async(q);
       if (pf) {
-        load_tile<K, GATHER, FULL>(a, tile_pos(tn < ntiles ? tn : t, tps), nvec, nxt);
+        load(tn < ntiles ? tn : t, nxt);
         __builtin_amdgcn_sched_barrier(0);
       } else {
-        load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, cur);
+        load(t, cur);
         __builtin_amdgcn_sched_barrier(0);  // all K loads in flight before the lookups
       }
       run(t, cur);
@@ -345,11 +368,11 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
         if (threadIdx.x == 0) {
           // >= K vector-memory ops (this step's loads) were issued after the
           // grab, so at most K outstanding means the grab has returned
-          if (slot == 0) publish<FULL ? K : 0, 0>(ring_base, g);
-          else publish<FULL ? K : 0, 4>(ring_base, g);
+          if (slot == 0) publish<QWAIT_K ? K : 0, 0>(ring_base, g);
+          else publish<QWAIT_K ? K : 0, 4>(ring_base, g);
         }
         ring_barrier();
-        const uint32_t nn = __builtin_amdgcn_readfirstlane(ring[slot]) * T;
+        const uint32_t nn = run_start(__builtin_amdgcn_readfirstlane(ring[slot]));
         slot ^= 1;
         rend = nrun + T < ntiles ? nrun + T : ntiles;
         nrun = nn;
@@ -360,7 +383,7 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
     if (t < ntiles) {
       if constexpr (PF) {
         u32x4 A[K], B[K];
-        load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
+        load(t, A);
         while (step(A, B, true) && step(B, A, true)) {
         }
       } else {
@@ -390,16 +413,16 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
   if (t >= tend) return;
   if constexpr (PF) {
     u32x4 A[K], B[K];
-    load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, A);
+    load(t, A);
     while (true) {
       const uint32_t tb = t + 1;
-      load_tile<K, GATHER, FULL>(a, tile_pos(tb < tend ? tb : t, tps), nvec, B);
+      load(tb < tend ? tb : t, B);
       __builtin_amdgcn_sched_barrier(0);
       run(t, A);
       if (tb >= tend) break;
       t = tb;
       const uint32_t ta = t + 1;
-      load_tile<K, GATHER, FULL>(a, tile_pos(ta < tend ? ta : t, tps), nvec, A);
+      load(ta < tend ? ta : t, A);
       __builtin_amdgcn_sched_barrier(0);
       run(t, B);
       if (ta >= tend) break;
@@ -408,7 +431,7 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
   } else {
     for (; t < tend; t++) {
       u32x4 d[K];
-      load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d);
+      load(t, d);
       run(t, d);
     }
   }
@@ -419,6 +442,21 @@ __device__ __forceinline__ void tile_loop(const MulArgs &a, const Body &body, ui
 // separate instantiation so encode/recover kernels carry no copy registers.
 // The queue ring lives in the dynamic LDS block after the tables (Q only
 // where it fits: queue_fits()).
+// Strided / gather geometry of a MulArgs launch: tile t = column tile
+// t % tps of stripe t / tps.
+template <int K, bool GATHER, bool FULL, bool PF, bool Q, class Body>
+__device__ __forceinline__ void mul_tiles(const MulArgs &a, const Body &body, uint32_t *ring) {
+  const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
+  const uint32_t tps = (nvec + kBlock - 1) / kBlock;
+  const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
+  auto load = [&](uint32_t t, u32x4(&d)[K]) { load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d); };
+  auto run = [&](uint32_t t, const u32x4(&d)[K]) {
+    const TilePos p = tile_pos(t, tps);
+    if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
+  };
+  tile_loop<K, PF, Q, FULL>(load, run, ntiles, a.queue_slot, a.tiles_per_grab, ring);
+}
+
 template <int K, int R, bool GATHER, bool COPY, bool FULL>
 __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
   constexpr bool PF = K <= ((COPY || !FULL) ? kPrefetchMaxKCopy : kPrefetchMaxK);
@@ -427,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void k_mul_vec(const MulArgs a) {
   extern __shared__ uint32_t tab[];
   Body::setup(a, tab);
   __syncthreads();
-  tile_loop<K, GATHER, FULL, PF, Q>(a, Body(tab), tab + Body::kLds / 4);
+  mul_tiles<K, GATHER, FULL, PF, Q>(a, Body(tab), tab + Body::kLds / 4);
 }
 
 template <int K, bool GATHER, bool COPY, bool FULL>
@@ -437,7 +475,64 @@ __global__ __launch_bounds__(kBlock) void k_mul_perm(const MulArgs a) {
   extern __shared__ uint32_t tab[];
   Body::setup(a, tab);
   __syncthreads();
-  tile_loop<K, GATHER, FULL, PF, true>(a, Body(tab), tab + Body::kLds / 4);
+  mul_tiles<K, GATHER, FULL, PF, true>(a, Body(tab), tab + Body::kLds / 4);
+}
+
+// --- ragged stripes (the last stripes of many objects) ---
+// Stripes of different chunk lengths in one launch, through the same
+// work-queue tile loop and LDS tables as k_mul_vec: tile t belongs to stripe
+// tile_stripe[t] (a device map built per call), column tile
+// t - stripe_tile0[s].  Every stripe is 16-byte aligned with 16-byte chunk
+// strides and len rounded up to 16 (the zero-padded tail arena of
+// nxec_encode_objects), so every lane moves whole 16-byte vectors.
+struct RaggedArgs {
+  const ListStripe *__restrict__ stripes;
+  const uint32_t *__restrict__ tile_stripe;
+  const uint32_t *__restrict__ stripe_tile0;
+  uint32_t ntiles;
+  int32_t k, rows, row0, queue_slot;
+  uint32_t tiles_per_grab;
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];
+};
+
+template <int K, int R>
+__global__ __launch_bounds__(kBlock) void k_mul_ragged(const RaggedArgs a) {
+  constexpr bool PF = K <= kPrefetchMaxKCopy;
+  constexpr int kLds = K * 1024 * R;
+  static_assert(queue_fits(kLds), "ragged kernels are queue-driven");
+  extern __shared__ uint32_t tab[];
+  build_tables<R>(a.coef, K, a.rows, tab);
+  __syncthreads();
+  const char *tl = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
+  auto where = [&](uint32_t t, ListStripe &st, uint32_t &v) {
+    const uint32_t s = a.tile_stripe[t];
+    st = a.stripes[s];
+    v = (t - a.stripe_tile0[s]) * kBlock + threadIdx.x;
+  };
+  auto load = [&](uint32_t t, u32x4(&d)[K]) {
+    ListStripe st;
+    uint32_t v;
+    where(t, st, v);
+    if (v * int64_t(16) < st.len) {
+#pragma unroll
+      for (int j = 0; j < K; j++) d[j] = ld_stream(st.src + j * st.src_cs + static_cast<size_t>(v) * 16);
+    }
+  };
+  auto run = [&](uint32_t t, const u32x4(&d)[K]) {
+    ListStripe st;
+    uint32_t v;
+    where(t, st, v);
+    if (v * int64_t(16) < st.len) {
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int j = 0; j < K; j++) lookup16<R>(tl + j * 1024 * R, d[j], acc);
+      store_rows_ptr(st.dst + a.row0 * st.dst_cs, st.dst_cs, a.rows, v, acc);
+    }
+  };
+  // wave 0 (lane 0 = the tile's first vector) always issues its K loads
+  tile_loop<K, PF, true, true>(load, run, a.ntiles, a.queue_slot, a.tiles_per_grab, tab + kLds / 4);
 }
 
 // Runtime-k vector kernel (k > kMaxTemplK), R = 1 tables, sources in groups of 4.
@@ -592,6 +687,58 @@ __global__ __launch_bounds__(256) void k_pad_copy(const PadCopy *items) {
   const int64_t per = ((it.dst_len + kPadParts - 1) / kPadParts + 15) / 16 * 16;
   const int64_t b0 = part * per, b1 = b0 + per < it.dst_len ? b0 + per : it.dst_len;
   for (int64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) it.dst[i] = i < it.src_len ? it.src[i] : 0;
+}
+
+// Last stripe of an object into the aligned tail arena: chunk j of the
+// stripe = object bytes [j*cl, (j+1)*cl) (zero past the object's remaining
+// rem bytes, chunk_manager.cc:390-399), written at dst + j*cls with
+// cls = cl rounded up to 16 and zeros in [cl, cls).  One thread per 16-byte
+// output vector; the 16 source bytes are assembled from dword-aligned loads
+// with v_alignbit (the source offset j*cl has any alignment), bytes where
+// the 20-byte window would leave the object.  Item i owns blocks
+// [bstart[i], bstart[i+1]) of kPadVecs*256 vectors (thread 0 finds the item).
+__global__ __launch_bounds__(256) void k_pad_chunks(const PadChunks *__restrict__ items,
+                                                    const uint32_t *__restrict__ bstart, int64_t nitems) {
+  __shared__ int64_t s_item;
+  if (threadIdx.x == 0) {
+    int64_t lo = 0, hi = nitems - 1;  // last item with bstart <= blockIdx.x
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (bstart[mid] <= blockIdx.x) lo = mid;
+      else hi = mid - 1;
+    }
+    s_item = lo;
+  }
+  __syncthreads();
+  const int64_t item = s_item;
+  const PadChunks it = items[item];
+  const int64_t vpc = it.cls / 16;  // vectors per chunk
+  const int64_t u0 = static_cast<int64_t>(blockIdx.x - bstart[item]) * (256 * kPadVecs);
+#pragma unroll
+  for (int r = 0; r < kPadVecs; r++) {
+    const int64_t u = u0 + r * 256 + threadIdx.x;  // output vector
+    if (u >= vpc * it.k) break;
+    const int64_t j = u / vpc, x = (u - j * vpc) * 16;  // chunk, byte offset in it
+    const int64_t sidx = j * it.cl + x;                 // source byte of output byte x
+    const int64_t nvalid = min(min(static_cast<int64_t>(16), it.cl - x), it.rem - sidx);  // may be <= 0
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (nvalid > 0) {
+      const uint8_t *sp = it.src + sidx;
+      const uintptr_t base = reinterpret_cast<uintptr_t>(sp) & ~uintptr_t(3);
+      if (nvalid == 16 && base + 20 <= reinterpret_cast<uintptr_t>(it.src + it.rem)) {
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(base);
+        const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 3) * 8;
+        const uint32_t r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+        w[0] = __builtin_amdgcn_alignbit(r1, r0, sb);
+        w[1] = __builtin_amdgcn_alignbit(r2, r1, sb);
+        w[2] = __builtin_amdgcn_alignbit(r3, r2, sb);
+        w[3] = __builtin_amdgcn_alignbit(r4, r3, sb);
+      } else {
+        for (int b = 0; b < nvalid; b++) w[b >> 2] |= static_cast<uint32_t>(sp[b]) << (8 * (b & 3));
+      }
+    }
+    st_stream(it.dst + j * it.cls + x, u32x4{w[0], w[1], w[2], w[3]});
+  }
 }
 
 __global__ void k_fill(uint8_t *p, int64_t bytes, uint64_t seed) {
@@ -857,6 +1004,60 @@ int launch_mul_list(int rows, int k, const uint8_t *coeffs, const ListStripe *d_
     if (e != hipSuccess) return hip_fail(e, "launch k_mul_list");
   }
   return NXEC_OK;
+}
+
+using RaggedFn = void (*)(RaggedArgs);
+template <int... Ks>
+constexpr std::array<RaggedFn, sizeof...(Ks)> ragged_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_mul_ragged<Ks + 1, (Ks + 1 <= 9 ? 16 : 8)>...}};
+}
+const std::array<RaggedFn, kMaxRaggedK> kRagged = ragged_table(std::make_integer_sequence<int, kMaxRaggedK>{});
+int ragged_lds(int k) { return k * 1024 * (k <= 9 ? 16 : 8) + kRingBytes; }
+
+int launch_mul_ragged(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const uint32_t *d_tile_stripe,
+                      const uint32_t *d_stripe_tile0, int64_t ntiles, int num_cus, void *stream) {
+  if (ntiles <= 0 || rows <= 0) return NXEC_OK;
+  if (k < 1 || k > kMaxRaggedK) return set_error(NXEC_ERR_INVALID, "ragged launch: k=%d unsupported", k);
+  if (ntiles >= (int64_t(1) << 32)) return set_error(NXEC_ERR_INVALID, "ragged launch: too many tiles");
+  static const bool raised = [] {
+    for (int kk = 1; kk <= kMaxRaggedK; kk++)
+      if (hipFuncSetAttribute(reinterpret_cast<const void *>(kRagged[kk - 1]),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, ragged_lds(kk)) != hipSuccess)
+        return false;
+    return true;
+  }();
+  if (!raised) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_ragged) failed");
+  const int64_t grid = std::min<int64_t>(num_cus, ntiles);
+  for (int r0 = 0; r0 < rows; r0 += kMaxRowsPerPass) {
+    RaggedArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.stripes = d_stripes;
+    a.tile_stripe = d_tile_stripe;
+    a.stripe_tile0 = d_stripe_tile0;
+    a.ntiles = static_cast<uint32_t>(ntiles);
+    a.k = k;
+    a.rows = rows - r0 < kMaxRowsPerPass ? rows - r0 : kMaxRowsPerPass;
+    a.row0 = r0;
+    a.queue_slot = static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
+    a.tiles_per_grab = std::max(1, std::min(8, (12 + k + a.rows - 1) / (k + a.rows)));
+    for (int r = 0; r < a.rows; r++)
+      for (int j = 0; j < k; j++) a.coef[r * k + j] = coeffs[static_cast<size_t>(r0 + r) * k + j];
+    hipLaunchKernelGGL(kRagged[k - 1], dim3(static_cast<unsigned>(grid)), dim3(kBlock), ragged_lds(k),
+                       static_cast<hipStream_t>(stream), a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "launch k_mul_ragged");
+  }
+  return NXEC_OK;
+}
+
+int launch_pad_chunks(const PadChunks *d_items, const uint32_t *d_bstart, int64_t nitems, int64_t nblocks,
+                      void *stream) {
+  if (nitems <= 0 || nblocks <= 0) return NXEC_OK;
+  if (nblocks >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "pad-chunks launch too large");
+  hipLaunchKernelGGL(k_pad_chunks, dim3(static_cast<unsigned>(nblocks)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     d_items, d_bstart, nitems);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_pad_chunks");
 }
 
 int launch_pad_copy(const PadCopy *d_items, int64_t nitems, void *stream) {

@@ -139,6 +139,72 @@ __device__ __forceinline__ void md5_stream(const uint8_t *p, int64_t nfull, uint
   }
 }
 
+// Misaligned chunks (p % 16 != 0: ragged last-stripe chunks of arbitrary
+// length packed back to back).  16-byte loads from the dword-aligned address
+// at or below p (global_load_dwordx4 needs only dword alignment on gfx950),
+// one extra dword per group, and every message word assembled with
+// v_alignbit over the lane's own byte shift.  Streams blocks [0, nblk); the
+// caller keeps nblk < the chunk's full-block count, so the extra dword after
+// the last streamed block is still inside the chunk.
+template <int D, int G>
+__device__ __forceinline__ void md5_stream_u(const uint8_t *p, int64_t nblk, uint32_t (&h)[4]) {
+  typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+  constexpr int W = 16 * G;  // dwords per group
+  const uint32_t *pd = reinterpret_cast<const uint32_t *>(p - (reinterpret_cast<uintptr_t>(p) & 3));
+  const uint32_t sb = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3) * 8;
+  auto load = [&](int64_t g, uint32_t(&raw)[W + 1]) {
+    const uint32_t *q = pd + g * W;
+#pragma unroll
+    for (int i = 0; i < W / 4; i++) {
+      const u32x4 v = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
+      raw[4 * i] = v.x;
+      raw[4 * i + 1] = v.y;
+      raw[4 * i + 2] = v.z;
+      raw[4 * i + 3] = v.w;
+    }
+    raw[W] = q[W];
+  };
+  auto hash = [&](const uint32_t(&raw)[W + 1], int nb) {
+#pragma unroll
+    for (int i = 0; i < G; i++) {
+      if (i < nb) {
+        uint32_t m[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) m[t] = __builtin_amdgcn_alignbit(raw[16 * i + t + 1], raw[16 * i + t], sb);
+        md5_block(h, m);
+      }
+    }
+  };
+  const int64_t ngroups = nblk / G;
+  if (ngroups > 0) {
+    uint32_t ring[D][W + 1];
+    const int64_t last = ngroups - 1;
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load(min(static_cast<int64_t>(j), last), ring[j]);
+    int64_t g = 0;
+    for (; g + D <= ngroups; g += D) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        load(min(g + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        hash(ring[j], G);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; j++)
+      if (g + j < ngroups) hash(ring[j], G);
+  }
+  const int rest = static_cast<int>(nblk - ngroups * G);  // < G blocks, in one final group
+  if (rest > 0) {
+    uint32_t raw[W + 1];
+    const uint32_t *q = pd + ngroups * W;
+#pragma unroll
+    for (int i = 0; i <= W; i++) raw[i] = i <= 16 * rest ? q[i] : 0u;
+    hash(raw, rest);
+  }
+}
+
 struct Md5Args {
   Md5Region r[kMaxMd5Regions];
   int64_t lane_end[kMaxMd5Regions];  // prefix sums of nchunks * nstripes
@@ -177,10 +243,16 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
   uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
   const int64_t nfull = len / 64;
   uint32_t m[16];
+  int64_t done = 0;  // full blocks hashed by a streaming path; the rest byte-wise
   if (aligned) {
     if (nfull > 0) md5_stream<D, G, NT>(p, nfull, h);
-  } else {
-    for (int64_t b = 0; b < nfull; b++) {
+    done = nfull;
+  } else if (nfull > 1) {
+    md5_stream_u<2, 4>(p, nfull - 1, h);
+    done = nfull - 1;
+  }
+  {
+    for (int64_t b = done; b < nfull; b++) {
 #pragma unroll
       for (int i = 0; i < 16; i++) {
         const uint8_t *q = p + b * 64 + 4 * i;

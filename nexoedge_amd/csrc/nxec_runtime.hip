@@ -501,7 +501,7 @@ int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int6
     int rc = nxec_object_layout(n, k, lengths[o], max_chunk_size, &ns, &nf, &cl);
     if (rc) return rc;
     *total_stripes += ns;
-    if (ns > nf) *tail_bytes += (int64_t(k) * cl + 15) / 16 * 16;
+    if (ns > nf) *tail_bytes += int64_t(k) * ((cl + 15) / 16 * 16);
   }
   return NXEC_OK;
 }
@@ -527,17 +527,27 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   nxec_gf_gen_rs_matrix(enc.data(), n, k);
   const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
 
-  // host plan: full stripes of every object as gather pointer tables (one fast
-  // launch), last stripes as padded copies + a variable-length list launch,
-  // every chunk an MD5 item; all tables go to the device in one copy
+  // Host plan, every table to the device in one copy:
+  //  * full stripes of every object: gather pointer tables, one k_mul_vec launch
+  //    (objects not 16-byte aligned: the byte-capable list kernel instead);
+  //  * each object's last stripe: its k chunks copied zero-padded into the
+  //    tail arena at 16-byte-aligned chunk strides (one k_pad_chunks launch),
+  //    then coded as aligned ragged stripes (one k_mul_ragged launch; the list
+  //    kernel when parity slots are not 16-byte aligned or k > 19);
+  //  * every chunk an MD5 item (one launch).
   std::vector<const uint8_t *> fsrc;
   std::vector<uint8_t *> fdst;
-  std::vector<PadCopy> pads;
-  std::vector<ListStripe> tails;
-  std::vector<int64_t> prefix(1, 0);
-  std::vector<Md5Item> items;
+  std::vector<PadChunks> pads;
+  std::vector<uint32_t> pad_bstart;
+  std::vector<ListStripe> ragged, ulist;
+  std::vector<uint32_t> stripe_tile0, tile_stripe;
+  std::vector<int64_t> uprefix(1, 0);
+  std::vector<Md5Item> items, ritems;
   bool full_aligned = M % 16 == 0;
-  int64_t g = 0, toff = 0;
+  // ragged stripes through the aligned work-queue kernel: parity slots must be
+  // 16-byte aligned (else they join the byte-capable list kernel)
+  const bool ragged_ok = p > 0 && M % 16 == 0 && (reinterpret_cast<uintptr_t>(d_parity) & 15) == 0 && k <= kMaxRaggedK;
+  int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
     nxec_object_layout(n, k, lengths[o], M, &ns, &nf, &cl);
@@ -553,54 +563,95 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
           for (int j = 0; j < k; j++) items.push_back({obj + (s * k + j) * M, M, dig + j * 16});
           for (int i = 0; i < p; i++) items.push_back({par + i * M, M, dig + (k + i) * 16});
         }
-      } else {  // last stripe: zero-padded copy to the tail arena (chunk_manager.cc:390-399)
+      } else {  // last stripe (chunk_manager.cc:390-399)
+        const int64_t cls = (cl + 15) / 16 * 16;
         uint8_t *td = d_tail + toff;
-        const int64_t rem = lengths[o] - nf * k * M;
-        pads.push_back({obj + nf * k * M, td, rem, int64_t(k) * cl});
-        tails.push_back({td, par, cl, cl, M});
-        prefix.push_back(prefix.back() + (cl + 15) / 16);
-        if (dig) {
-          for (int j = 0; j < k; j++) items.push_back({td + j * cl, cl, dig + j * 16});
-          for (int i = 0; i < p; i++) items.push_back({par + i * M, cl, dig + (k + i) * 16});
+        pads.push_back({obj + nf * k * M, td, lengths[o] - nf * k * M, cl, cls, k});
+        pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
+        pad_blocks += (cls / 16 * k + 256 * kPadVecs - 1) / (256 * kPadVecs);
+        if (p > 0 && !ragged_ok) {
+          ulist.push_back({td, par, cl, cls, M});
+          uprefix.push_back(uprefix.back() + (cl + 15) / 16);
+        } else if (p > 0) {
+          const uint32_t s_idx = static_cast<uint32_t>(ragged.size());
+          ragged.push_back({td, par, cls, cls, M});
+          stripe_tile0.push_back(static_cast<uint32_t>(tile_stripe.size()));
+          const int64_t nt = (cls / 16 + 1023) / 1024;
+          for (int64_t t = 0; t < nt; t++) tile_stripe.push_back(s_idx);
         }
-        toff += (int64_t(k) * cl + 15) / 16 * 16;
+        if (dig) {
+          for (int j = 0; j < k; j++) ritems.push_back({td + j * cls, cl, dig + j * 16});
+          for (int i = 0; i < p; i++) ritems.push_back({par + i * M, cl, dig + (k + i) * 16});
+        }
+        toff += k * cls;
       }
     }
   }
+  // MD5 lanes in descending chunk length: a wave lasts as long as its longest
+  // chain, and the first waves dispatched get a SIMD to themselves, so full
+  // chunks go first and the last-stripe chunks follow longest first (sorted by
+  // object, k + p items per object share one length)
+  {
+    const size_t per = static_cast<size_t>(n);
+    std::vector<size_t> order(ritems.size() / per);
+    for (size_t i = 0; i < order.size(); i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](size_t x, size_t y) { return ritems[x * per].len > ritems[y * per].len; });
+    for (size_t o : order) items.insert(items.end(), ritems.begin() + o * per, ritems.begin() + (o + 1) * per);
+  }
+  if (pad_blocks >= (int64_t(1) << 31) || tile_stripe.size() >= (size_t(1) << 32))
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_objects: batch too large (split it)");
+  pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
   const int64_t nfs = static_cast<int64_t>(fsrc.size()) / k;
-  // full stripes of unaligned objects go through the list kernel instead
-  if (!full_aligned && nfs > 0) {
+  if (!full_aligned && nfs > 0 && p > 0) {  // unaligned objects: full stripes through the list kernel too
     for (int64_t f = 0; f < nfs; f++) {
-      tails.push_back({fsrc[f * k], p > 0 ? fdst[f * p] : nullptr, M, M, M});
-      prefix.push_back(prefix.back() + (M + 15) / 16);
+      ulist.push_back({fsrc[f * k], fdst[f * p], M, M, M});
+      uprefix.push_back(uprefix.back() + (M + 15) / 16);
     }
   }
-  const size_t b_fsrc = fsrc.size() * sizeof(void *), b_fdst = fdst.size() * sizeof(void *);
-  const size_t b_pads = pads.size() * sizeof(PadCopy), b_tails = tails.size() * sizeof(ListStripe);
-  const size_t b_pref = prefix.size() * sizeof(int64_t), b_items = items.size() * sizeof(Md5Item);
-  size_t off[7] = {0};
-  const size_t sizes[6] = {b_fsrc, b_fdst, b_pads, b_tails, b_pref, b_items};
-  for (int i = 0; i < 6; i++) off[i + 1] = off[i] + (sizes[i] + 15) / 16 * 16;
+  struct Tab {
+    const void *h;
+    size_t bytes;
+  };
+  const Tab tabs[] = {{fsrc.data(), fsrc.size() * sizeof(void *)},
+                      {fdst.data(), fdst.size() * sizeof(void *)},
+                      {pads.data(), pads.size() * sizeof(PadChunks)},
+                      {pad_bstart.data(), pad_bstart.size() * sizeof(uint32_t)},
+                      {ragged.data(), ragged.size() * sizeof(ListStripe)},
+                      {stripe_tile0.data(), stripe_tile0.size() * sizeof(uint32_t)},
+                      {tile_stripe.data(), tile_stripe.size() * sizeof(uint32_t)},
+                      {ulist.data(), ulist.size() * sizeof(ListStripe)},
+                      {uprefix.data(), uprefix.size() * sizeof(int64_t)},
+                      {items.data(), items.size() * sizeof(Md5Item)}};
+  constexpr int kTabs = sizeof(tabs) / sizeof(tabs[0]);
+  size_t off[kTabs + 1] = {0};
+  for (int i = 0; i < kTabs; i++) off[i + 1] = off[i] + (tabs[i].bytes + 15) / 16 * 16;
   Slot *slot = nullptr;
-  rc = acquire_slot(ctx, std::max<size_t>(off[6], 16), &slot);
+  rc = acquire_slot(ctx, std::max<size_t>(off[kTabs], 16), &slot);
   if (rc) return rc;
-  const void *srcs[6] = {fsrc.data(), fdst.data(), pads.data(), tails.data(), prefix.data(), items.data()};
   // the slot's staging may still be in use by an earlier call on its own stream
   rc = hip_check(hipStreamSynchronize(slot->stream), "slot sync");
-  for (int i = 0; i < 6 && !rc; i++)
-    if (sizes[i]) std::memcpy(slot->h + off[i], srcs[i], sizes[i]);
-  if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[6], hipMemcpyHostToDevice, st), "tables H2D");
+  for (int i = 0; i < kTabs && !rc; i++)
+    if (tabs[i].bytes) std::memcpy(slot->h + off[i], tabs[i].h, tabs[i].bytes);
+  if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[kTabs], hipMemcpyHostToDevice, st), "tables H2D");
   auto dptr = [&](int i) { return slot->d + off[i]; };
   if (!rc && p > 0 && full_aligned && nfs > 0)
     rc = stripes_mul_impl(ctx, p, k, prow, nullptr, reinterpret_cast<const unsigned char *const *>(dptr(0)), nullptr,
                           0, 0, nullptr, reinterpret_cast<unsigned char *const *>(dptr(1)), nullptr, 0, 0, nullptr, M,
                           nfs, st);
-  if (!rc) rc = launch_pad_copy(reinterpret_cast<const PadCopy *>(dptr(2)), int64_t(pads.size()), st);
-  if (!rc && p > 0)
-    rc = launch_mul_list(p, k, prow, reinterpret_cast<const ListStripe *>(dptr(3)),
-                         reinterpret_cast<const int64_t *>(dptr(4)), int64_t(tails.size()), prefix.back(),
+  if (!rc)
+    rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
+                           int64_t(pads.size()), pad_blocks, st);
+  // after the pad copy on the same stream: the tail arena is complete
+  if (!rc && !ragged.empty())
+    rc = launch_mul_ragged(p, k, prow, reinterpret_cast<const ListStripe *>(dptr(4)),
+                           reinterpret_cast<const uint32_t *>(dptr(6)), reinterpret_cast<const uint32_t *>(dptr(5)),
+                           int64_t(tile_stripe.size()), ctx->num_cus, st);
+  if (!rc && !ulist.empty())
+    rc = launch_mul_list(p, k, prow, reinterpret_cast<const ListStripe *>(dptr(7)),
+                         reinterpret_cast<const int64_t *>(dptr(8)), int64_t(ulist.size()), uprefix.back(),
                          ctx->num_cus, st);
-  if (!rc && !items.empty()) rc = launch_md5_list(reinterpret_cast<const Md5Item *>(dptr(5)), int64_t(items.size()), st);
+  if (!rc && !items.empty()) rc = launch_md5_list(reinterpret_cast<const Md5Item *>(dptr(9)), int64_t(items.size()), st);
   // the tables live in the slot: drain before handing it back (synchronous call)
   const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
   release_slot(ctx, slot);

@@ -546,12 +546,13 @@ def test_survey_named_encode_entry_points(gpu_ctx):
     pb.free()
 
 
-@pytest.mark.parametrize("misalign", [0, 3])
-def test_encode_objects_matches_per_object(gpu_ctx, misalign):
+@pytest.mark.parametrize("misalign,n,k,M", [(0, 9, 6, 4096), (3, 9, 6, 4096), (0, 9, 6, 1000), (0, 14, 10, 65536),
+                                             (5, 14, 10, 16400), (0, 24, 20, 4096)])
+def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
     """Many objects per call (full stripes in one gather launch, last stripes in
-    one variable-length launch, MD5 of every chunk in one list launch) equals
-    encoding each object on its own with nxec_encode_object."""
-    n, k, M = 9, 6, 4096
+    one ragged work-queue launch -- the list kernel for k > 19 --, MD5 of every
+    chunk in one list launch) equals encoding each object on its own with
+    nxec_encode_object; the tail arena holds the zero-padded last-stripe chunks."""
     p = n - k
     lengths = [0, 1, 17, k * M - 1, k * M, 3 * k * M + 100, 5000, 2 * k * M, 12345]
     total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
@@ -570,11 +571,21 @@ def test_encode_objects_matches_per_object(gpu_ctx, misalign):
     gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
     gp = par.download().reshape(total, p, M)
     gm = md5.download().reshape(total, n, 16)
-    g = 0
+    gt = tail.download()
+    g, toff = 0, 0
     for i, (o, L) in enumerate(zip(offs, lengths)):
         ns, nf, cl = nxec.object_layout(n, k, L, M)
         if ns == 0:
             continue
+        if ns > nf:  # tail arena: zero-padded chunks at 16-byte-aligned strides
+            cls = (cl + 15) // 16 * 16
+            rem = host[o + nf * k * M:o + L]
+            want = np.zeros(k * cl, dtype=np.uint8)
+            want[:len(rem)] = rem
+            got = gt[toff:toff + k * cls].reshape(k, cls)
+            assert np.array_equal(got[:, :cl], want.reshape(k, cl)), i
+            assert not got[:, cl:].any(), i
+            toff += k * cls
         ob = up(host[o:o + L])
         op, ot, om = nxec.DeviceBuffer(ns * p * M), nxec.DeviceBuffer(k * M), nxec.DeviceBuffer(ns * n * 16)
         gpu_ctx.encode_object(n, k, ob.ptr, L, M, op.ptr, ot.ptr, om.ptr)

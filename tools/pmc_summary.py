@@ -2,7 +2,7 @@
 """Summarise separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
 bench.py into profiles/rNN_pmc_traffic.json (HBM bytes per launch of the
 headline kernel), applying the gfx950 FETCH_SIZE x2 correction of
-MI355X_MICROARCH.md.  Usage: pmc_summary.py OUT_DIR ALGORITHMIC_BYTES > json"""
+MI355X_MICROARCH.md.  Usage: pmc_summary.py OUT_DIR ALGORITHMIC_BYTES [KERNEL_SUBSTRING] > json"""
 import csv
 import json
 import sys
@@ -15,7 +15,7 @@ def per_launch_kb(path, kernel_sub):
 
 def main():
     out, alg = sys.argv[1], int(sys.argv[2])
-    sub = "k_mul_vec<10, 16, false, false, true>"
+    sub = sys.argv[3] if len(sys.argv) > 3 else "k_mul_vec<10, 8, false, false, true>"
     f, nf = per_launch_kb(f"{out}/pmc_FETCH_SIZE/run_counter_collection.csv", sub)
     w, nw = per_launch_kb(f"{out}/pmc_WRITE_SIZE/run_counter_collection.csv", sub)
     rd, wr = int(2 * f * 1024), int(w * 1024)
