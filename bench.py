@@ -160,10 +160,16 @@ def cpu_baseline(args, n, k, cs):
 
 
 def load_traffic(path, launch_bytes):
+    """HBM bytes per launch from the committed PMC summary (profiles/rNN_pmc_traffic.json,
+    measured on the 4096-stripe headline launch); for another batch size the
+    measured traffic/algorithmic ratio is applied to this launch's bytes."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+        hbm, alg = d.get("hbm_bytes_per_launch"), d.get("algorithmic_bytes_per_launch")
+        if hbm is None or not alg:
+            return None
+        return hbm if alg == launch_bytes else int(round(hbm / alg * launch_bytes))
     except (OSError, ValueError):
         return None
 
@@ -343,7 +349,9 @@ def main():
     args = parse()
     grp = RankGroup()
     world, rank, local = grp.world, grp.rank, grp.local_rank
-    ctx = nxec.Context(local)
+    # one rank per GPU; more ranks than visible GPUs share them round-robin
+    # (only for rehearsing the multi-rank path on a small box)
+    ctx = nxec.Context(local % max(1, nxec.device_count()))
     stream = ctx.stream
     wl = WORKLOADS[args.workload](args, ctx, stream, rank)
     step_bytes = sum(b for _, _, b in wl.ops)
