@@ -600,3 +600,34 @@ def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
             b.free()
     for b in (arena, par, tail, md5):
         b.free()
+
+
+def test_tile_queue_slots_wrap_and_streams(gpu_ctx):
+    """Work-queue kernels draw one counter slot per launch from a 4096-slot
+    device ring and the last workgroup resets it: 4300 consecutive launches
+    (every slot reused) alternating between two streams must all produce
+    complete, bit-exact parity."""
+    n, k, cs, ns = 14, 10, 65536, 3  # 12 tiles per launch: fewer tiles than workgroups
+    data = [fill_bytes(k * cs, 9100 + s) for s in range(ns)]
+    buf, host = stripe_buffer(n, k, cs, cs, data)
+    want = np.stack([np.stack(oracle.matmul(nxec.gen_rs_matrix(n, k)[k:], list(d.reshape(k, cs)))) for d in data])
+    lib = nxec.lib
+    s2 = C.c_void_p()
+    assert lib.nxec_stream_create(C.byref(s2)) == 0
+    try:
+        for i in range(4300):
+            if i % 500 == 0 or i == 4290:
+                gpu_ctx.sync()
+                assert lib.nxec_stream_sync(s2) == 0
+                z = host.copy()
+                z[:, k:] = 0
+                buf.upload(z)  # clear parity so a skipped tile cannot pass
+            gpu_ctx.rs_encode(n, k, buf.ptr, cs, n * cs, cs, ns, s2 if i % 2 else None)
+            if i % 500 == 499 or i == 4299:
+                gpu_ctx.sync()
+                assert lib.nxec_stream_sync(s2) == 0
+                got = buf.download().reshape(ns, n, cs)[:, k:]
+                assert np.array_equal(got, want), i
+    finally:
+        lib.nxec_stream_destroy(s2)
+        buf.free()
