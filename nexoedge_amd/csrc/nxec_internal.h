@@ -40,6 +40,7 @@ struct MulArgs {
   int32_t dst_ptr_rows;             // gather mode: rows_total
   int32_t queue_slot;               // tile-queue slot of this launch (set by launch_mul)
   uint32_t tiles_per_grab;          // work-queue run length (set by launch_mul)
+  uint32_t stripe_group;            // tiles column-major within groups of this many stripes (1 = stripe-major)
   // strided form: byte offsets of the chunks inside a stripe (idx * chunk_stride,
   // precomputed on the host; < 4 GiB so they stay single 32-bit SGPRs)
   uint32_t src_off[NXEC_MAX_K + 1];

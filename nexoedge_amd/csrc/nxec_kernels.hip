@@ -28,6 +28,7 @@
 //  * No MFMA: this is byte-wise lookup/XOR work bounded by HBM bandwidth.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <cstdlib>
@@ -172,6 +173,16 @@ struct TilePos {
 __device__ __forceinline__ TilePos tile_pos(uint32_t t, uint32_t tps) {
   const uint32_t s = t / tps;
   return {s, (t - s * tps) * kBlock + threadIdx.x};
+}
+// With stripe groups of sg > 1, tiles run column-major inside each group of
+// sg consecutive stripes (the last group may be smaller).
+__device__ __forceinline__ TilePos tile_pos(uint32_t t, uint32_t tps, uint32_t sg, uint32_t nstripes) {
+  if (sg <= 1) return tile_pos(t, tps);
+  const uint32_t per = sg * tps;
+  const uint32_t g = t / per, w = t - g * per;
+  const uint32_t gs = nstripes - g * sg < sg ? nstripes - g * sg : sg;
+  const uint32_t c = w / gs;
+  return {g * sg + (w - c * gs), c * kBlock + threadIdx.x};
 }
 
 // FULL: every tile is complete (vec_count % kBlock == 0), so no lane predicate
@@ -449,9 +460,10 @@ __device__ __forceinline__ void mul_tiles(const MulArgs &a, const Body &body, ui
   const uint32_t nvec = static_cast<uint32_t>(a.vec_count);
   const uint32_t tps = (nvec + kBlock - 1) / kBlock;
   const uint32_t ntiles = tps * static_cast<uint32_t>(a.nstripes);
-  auto load = [&](uint32_t t, u32x4(&d)[K]) { load_tile<K, GATHER, FULL>(a, tile_pos(t, tps), nvec, d); };
+  const uint32_t sg = a.stripe_group, ns = static_cast<uint32_t>(a.nstripes);
+  auto load = [&](uint32_t t, u32x4(&d)[K]) { load_tile<K, GATHER, FULL>(a, tile_pos(t, tps, sg, ns), nvec, d); };
   auto run = [&](uint32_t t, const u32x4(&d)[K]) {
-    const TilePos p = tile_pos(t, tps);
+    const TilePos p = tile_pos(t, tps, sg, ns);
     if (FULL || p.v < nvec) body(a, p.s, static_cast<uint32_t>(a.vec_begin) + p.v, d);
   };
   tile_loop<K, PF, Q, FULL>(load, run, ntiles, a.queue_slot, a.tiles_per_grab, ring);
@@ -958,6 +970,12 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
       MulArgs b = a;
       b.queue_slot = static_order() ? -1 : static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
       b.tiles_per_grab = tiles_per_grab(b);
+      // chunks of >= 2 MiB: walk groups of 8 stripes column-major, so the
+      // in-flight window spans 8 stripes like it does at 1 MiB (4 MiB chunk
+      // stride: 0.655 -> 0.711 of 8 TB/s; 2 MiB neutral; 1 MiB and below stay
+      // stripe-major, profiles/r01_chunk_stride_group.log)
+      b.stripe_group = (b.vec_count + kBlock - 1) / kBlock >= 128 ? 8 : 1;
+      if (const char *e = std::getenv("NXEC_STRIPE_GROUP")) b.stripe_group = static_cast<uint32_t>(std::max(1, std::atoi(e)));
       b.vec_begin = a.vec_begin + parts[pi][0];
       b.vec_count = parts[pi][1];
       const bool is_full = pi == 0;

@@ -631,3 +631,16 @@ def test_tile_queue_slots_wrap_and_streams(gpu_ctx):
     finally:
         lib.nxec_stream_destroy(s2)
         buf.free()
+
+
+@pytest.mark.parametrize("ns", [1, 9, 19])
+def test_large_chunk_stripe_groups(gpu_ctx, ns):
+    """Chunks >= 2 MiB run column-major inside groups of 8 stripes (the last
+    group partial): every stripe's parity still matches the oracle."""
+    n, k, cs = 6, 4, (2 << 20) + 4096
+    data = [fill_bytes(k * cs, 7700 + s) for s in range(ns)]
+    out = run_encode(gpu_ctx, n, k, cs, cs, data)
+    enc = nxec.gen_rs_matrix(n, k)[k:]
+    for s in range(ns):
+        want = oracle.matmul(enc, list(data[s].reshape(k, cs)))
+        assert all(np.array_equal(out[s, k + r], want[r]) for r in range(n - k)), s

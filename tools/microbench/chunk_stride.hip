@@ -60,7 +60,8 @@ int main(int argc, char **argv) {
         tot += ms;
       }
       const double bytes = (double)ns * n * cs, ms = tot / reps;
-      printf("cs %5ld KiB pad %6ld  stripes %6ld  %7.3f ms  %7.1f GB/s  frac8T %.3f\n", (long)(cs >> 10), (long)pad,
+      const char *sgv = getenv("NXEC_STRIPE_GROUP");
+      printf("sg %-2s cs %5ld KiB pad %6ld  stripes %6ld  %7.3f ms  %7.1f GB/s  frac8T %.3f\n", sgv ? sgv : "1", (long)(cs >> 10), (long)pad,
              (long)ns, ms, bytes / (ms * 1e-3) / 1e9, bytes / (ms * 1e-3) / 8e12);
       fflush(stdout);
     }

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(1024) void k_phase(const Args a) {
 // (workgroup b runs on XCD b % 8 under round-robin placement), each owning a
 // contiguous eighth of the tiles.  PF: next tile's loads issued before this
 // tile's stores.
-template <int K, int ROWS, int BLOCK, int G, bool XCD, bool PF>
+template <int K, int ROWS, int BLOCK, int G, bool XCD, bool PF, int LP = 1, int SP = 1>
 __global__ __launch_bounds__(BLOCK) void k_queue(const Args a) {
   constexpr uint32_t kTile = BLOCK * 16;
   __shared__ uint32_t s_next[2];
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(BLOCK) void k_queue(const Args a) {
     const uint32_t s = tt / tps;
     const uint8_t *sp = a.buf + s * sstride + (tt - s * tps) * kTile;
 #pragma unroll
-    for (int j = 0; j < K; j++) d[j] = ld<1>(sp + j * a.cs, threadIdx.x * 16);
+    for (int j = 0; j < K; j++) d[j] = ld<LP>(sp + j * a.cs, threadIdx.x * 16);
   };
   auto body = [&](uint32_t tt, const u32x4(&d)[K]) {
     const uint32_t s = tt / tps;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(BLOCK) void k_queue(const Args a) {
     for (int j = 1; j < K; j++) xx ^= d[j];
     uint8_t *dp = a.buf + s * sstride + K * a.cs + (tt - s * tps) * kTile;
 #pragma unroll
-    for (int r = 0; r < ROWS; r++) st<1>(dp + r * a.cs, threadIdx.x * 16, xx + static_cast<unsigned>(r));
+    for (int r = 0; r < ROWS; r++) st<SP>(dp + r * a.cs, threadIdx.x * 16, xx + static_cast<unsigned>(r));
   };
   while (t < hi) {
     if (threadIdx.x == 0) s_next[par ^ 1] = lo + atomicAdd(q, 1u) * G;
@@ -433,16 +433,21 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_queue<10, 4, BLOCK, G, XCDQ, PF>), dim3(ncu * WPC), dim3(BLOCK), 0, 0, a);           \
   })
   QUEUE_VARIANT(1024, 1, false, false, 1);
-  QUEUE_VARIANT(1024, 1, true, false, 1);
-  QUEUE_VARIANT(1024, 2, false, false, 1);
-  QUEUE_VARIANT(1024, 2, false, true, 1);
-  QUEUE_VARIANT(1024, 4, false, true, 1);
-  QUEUE_VARIANT(1024, 4, true, true, 1);
-  QUEUE_VARIANT(1024, 8, true, true, 1);
-  QUEUE_VARIANT(512, 1, false, false, 2);
-  QUEUE_VARIANT(512, 2, true, true, 2);
-  QUEUE_VARIANT(256, 1, true, false, 4);
-  QUEUE_VARIANT(1024, 1, false, false, 2);
+#define QPOL(LP, SP)                                                                                              \
+  timeit("queue G1 LP" #LP " SP" #SP, bytes, [&] {                                                               \
+    CHECK(hipMemsetAsync(queue, 0, 1024, 0));                                                                   \
+    hipLaunchKernelGGL((k_queue<10, 4, 1024, 1, false, false, LP, SP>), dim3(ncu), dim3(1024), 0, 0, a);       \
+  })
+  QPOL(0, 0);
+  QPOL(0, 1);
+  QPOL(1, 0);
+  QPOL(2, 1);
+  QPOL(3, 1);
+  QPOL(1, 2);
+  QPOL(1, 3);
+  QPOL(3, 3);
+  QPOL(2, 2);
+  QUEUE_VARIANT(1024, 1, false, false, 1);
   CHECK(hipFree(buf));
   return 0;
 }
