@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--cpu-stripes", type=int, default=192)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="min wall time of the SIMD CPU baseline leg")
     ap.add_argument("--cpu-ref-stripes", type=int, default=96, help="stripes for the (slow) reference base-C leg")
-    ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D->encode->D2H pipeline")
+    ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true", default=True,
+                    help="also time the pinned H2D->encode->D2H pipeline (default on; N=1 headline workload only)")
+    ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
     ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files"]), default="rs10_4",
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
@@ -447,9 +449,10 @@ def main():
         if wl.name == "rs10_4":
             k, cs = args.k, args.chunk
             result["user_data_gib_s"] = round(2 * wl.stripes * k * cs * args.steps * world / elapsed / GIB, 2)
-    if args.host_inclusive and rank == 0:
+    headline_n1 = rank == 0 and world == 1 and wl.name == "rs10_4"
+    if args.host_inclusive and headline_n1:
         result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.name == "rs10_4":
+    if headline_n1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.n, args.k, args.chunk)
         if args.host_inclusive:
             result["cpu_baseline"]["write_path_with_md5"] = cpu_write_path(args, args.n, args.k, args.chunk)
