@@ -644,3 +644,61 @@ def test_large_chunk_stripe_groups(gpu_ctx, ns):
     for s in range(ns):
         want = oracle.matmul(enc, list(data[s].reshape(k, cs)))
         assert all(np.array_equal(out[s, k + r], want[r]) for r in range(n - k)), s
+
+
+@pytest.mark.parametrize("failed", [0, 15])
+def test_rs12_4_full_batch_repair(gpu_ctx, failed):
+    """Config 4 at its full size (RS(12,4), 1 MiB chunks, 4096 stripes): after
+    erasing one chunk per stripe, both the fused recover and the CAR path
+    (racks of 4 chunks: partial encodes + XOR finalize) restore the batch
+    checksum; sampled stripes bit-exact vs the oracle."""
+    n, k, cs, ns, g = 16, 12, 1 << 20, 4096, 4
+    stripe = n * cs
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(4242 + failed)
+    gpu_ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns)
+    gpu_ctx.sync()
+    full = buf.checksum()
+    racks = [list(range(r, min(r + g, n))) for r in range(0, n, g)]
+    G = len(nxec.car_plan(n, k, failed, racks))
+    part = nxec.DeviceBuffer(ns * G * cs)
+    for path in ("fused", "car"):
+        erase_chunks(gpu_ctx, buf, n, cs, ns, [failed])
+        assert buf.checksum() != full
+        if path == "fused":
+            gpu_ctx.rs_recover(n, k, [failed], buf.ptr, cs, stripe, cs, ns)
+        else:
+            gpu_ctx.rs_car_repair(n, k, failed, racks, buf.ptr, cs, stripe, part.ptr, cs, G * cs, cs, ns)
+        gpu_ctx.sync()
+        assert buf.checksum() == full, path
+    for s in (0, 2049, 4095):
+        h = buf.download(stripe, offset=s * stripe).reshape(n, cs)
+        want = oracle.matmul(nxec.gen_rs_matrix(n, k)[k:], list(h[:k]))
+        assert all(np.array_equal(h[k + r], want[r]) for r in range(n - k)), s
+    part.free()
+    buf.free()
+
+
+@pytest.mark.parametrize("cs", [65536, 262144, 1 << 20, 4 << 20])
+def test_rs16_4_full_batch_mixed(gpu_ctx, cs):
+    """Config 5 at its full per-GPU size (RS(16,4), ~32 GiB of stripes per chunk
+    size): encode, then every 4-erasure pattern of the bench recovers the batch
+    checksum; first/last stripes bit-exact vs the oracle."""
+    n, k = 20, 16
+    stripe = n * cs
+    ns = (32 << 30) // stripe
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(1600 + cs)
+    gpu_ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns)
+    gpu_ctx.sync()
+    full = buf.checksum()
+    for failed in ([0, 1, 2, 3], [16, 17, 18, 19], [1, 4, 17, 19]):
+        erase_chunks(gpu_ctx, buf, n, cs, ns, failed)
+        gpu_ctx.rs_recover(n, k, failed, buf.ptr, cs, stripe, cs, ns)
+        gpu_ctx.sync()
+        assert buf.checksum() == full, failed
+    for s in (0, ns - 1):
+        h = buf.download(stripe, offset=s * stripe).reshape(n, cs)
+        want = oracle.matmul(nxec.gen_rs_matrix(n, k)[k:], list(h[:k]))
+        assert all(np.array_equal(h[k + r], want[r]) for r in range(n - k)), s
+    buf.free()
