@@ -39,6 +39,12 @@ $(LIBDIR)/libnxec.so: $(LIB_OBJS)
 oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_oracle.h
 	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c oracle/nxec_cpu_simd.c -o $@ -lpthread
 
+# drop-in per-stripe rate through the C++ surface (tools/dropin_rate.cc)
+tools: build/dropin_rate
+build/dropin_rate: tools/dropin_rate.cc $(LIBDIR)/libnxec.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread -o $@
+
 # design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
 tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling tools/microbench/mem_pattern tools/microbench/chunk_stride
 tools/microbench/shape_ceiling: tools/microbench/shape_ceiling.hip $(LIBDIR)/libnxec.so
@@ -61,4 +67,4 @@ golden: ref
 clean:
 	rm -rf build $(LIBDIR)/libnxec.so oracle/liboracle.so
 
-.PHONY: all ref golden clean tune
+.PHONY: all ref golden clean tune tools

@@ -3,6 +3,8 @@
 // kernels (nxec_encode_host / nxec_encode_host_ex), host code only plans.
 #include "rs.hh"
 
+#include "nxec_internal.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -46,13 +48,12 @@ bool RSCode::encode(data_t *data, length_t dataSize, std::vector<Chunk> &stripe,
       stripe.clear();
       return false;
     }
-    if (i < k) {
-      std::memcpy(stripe.at(i).data, data + static_cast<size_t>(i) * cs, cs);
-      datap[i] = stripe.at(i).data;
-    } else {
-      codep[i - k] = stripe.at(i).data;
-    }
+    if (i < k) datap[i] = stripe.at(i).data;
+    else codep[i - k] = stripe.at(i).data;
   }
+  // rs.cc:80's copy of the data into the chunks, spread over the library's
+  // host pool (fresh chunk buffers fault their pages in on first touch)
+  nxec::host_parallel_for(k, [&](int i) { std::memcpy(stripe[i].data, data + static_cast<size_t>(i) * cs, cs); });
   if (n == k || cs == 0) return true;
   const int rc = nxec_encode_host(static_cast<int>(cs), k, n - k, _encodeMatrix + k * k, datap.data(), codep.data());
   if (rc != NXEC_OK) {

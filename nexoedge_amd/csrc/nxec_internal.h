@@ -3,11 +3,16 @@
 #define NXEC_INTERNAL_H
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "nxec.h"
 
 namespace nxec {
+
+// Runs fn(i) for i in [0, n) on the library's host worker pool (staging
+// copies of the host entry points); returns when all are done.
+void host_parallel_for(int n, const std::function<void(int)> &fn);
 
 // Sets the calling thread's last-error message and returns `code`.
 int set_error(int code, const char *fmt, ...);
@@ -18,6 +23,7 @@ int repair_rows(int n, int k, const std::vector<uint8_t> &enc, const int32_t *in
 constexpr int kMaxRowsPerPass = 4;  // one packed 32-bit LDS entry holds 4 row products
 constexpr int kQueueSlots = 4096;   // per-launch tile-queue slots (device ring, see nxec_kernels.hip)
 constexpr uint32_t kNoCopy = 0xFFFFFFFFu;
+constexpr int64_t kHostPiece = 256 * 1024;  // column piece of the pipelined host entry points
 
 // Kernel arguments of one GF(2^8) stripe-multiply pass (<= 4 output rows).
 // Chunk (s, c) of the source lives at src + s*src_stripe_stride + c*src_chunk_stride

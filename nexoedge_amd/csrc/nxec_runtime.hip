@@ -4,14 +4,19 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nxec.h"
@@ -30,8 +35,99 @@ struct Slot {
   uint8_t *h = nullptr;
   uint8_t *d = nullptr;
   size_t cap = 0;
+  std::vector<hipEvent_t> events;  // per-piece completion (pipelined host path)
 };
+
+// Host worker pool for staging copies (pageable <-> pinned) of the host entry
+// points: one memcpy thread moves ~10 GB/s, so a 1 MiB RS(10,4) stripe spends
+// most of a call copying.  parallel_for splits a call's copies over the pool;
+// the calling thread works too, and concurrent callers share the pool.
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool pool;
+    return pool;
+  }
+  // runs fn(i) for i in [0, n), returns when all are done.  The pool serves
+  // one job at a time: a caller arriving while it is busy (many concurrent
+  // callers already keep the cores busy) runs its items inline.
+  void parallel_for(int n, const std::function<void(int)> &fn) {
+    if (n <= 0) return;
+    bool expected = false;
+    if (n == 1 || workers_.empty() || !busy_.compare_exchange_strong(expected, true)) {
+      for (int i = 0; i < n; i++) fn(i);
+      return;
+    }
+    struct Release {
+      std::atomic<bool> &b;
+      ~Release() { b.store(false); }
+    } release{busy_};
+    struct Job {
+      const std::function<void(int)> *fn;
+      std::atomic<int> next{0}, done{0};
+      int n;
+    };
+    auto job = std::make_shared<Job>();
+    job->fn = &fn;
+    job->n = n;
+    auto work = [job] {
+      int i;
+      while ((i = job->next.fetch_add(1)) < job->n) {
+        (*job->fn)(i);
+        job->done.fetch_add(1, std::memory_order_release);
+      }
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      const int helpers = std::min<int>(n - 1, static_cast<int>(workers_.size()));
+      for (int h = 0; h < helpers; h++) tasks_.push_back(work);
+    }
+    cv_.notify_all();
+    work();
+    while (job->done.load(std::memory_order_acquire) < n) std::this_thread::yield();
+  }
+
+ private:
+  HostPool() {
+    int nt = 8;
+    if (const char *e = std::getenv("NXEC_HOST_THREADS")) nt = std::max(0, std::atoi(e));
+    for (int i = 0; i < nt; i++) workers_.emplace_back([this] { loop(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : workers_) t.join();
+  }
+  void loop() {
+    while (true) {
+      std::function<void()> t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || !tasks_.empty(); });
+        if (stop_ && tasks_.empty()) return;
+        t = std::move(tasks_.front());
+        tasks_.pop_front();
+      }
+      t();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> tasks_;
+  std::vector<std::thread> workers_;
+  std::atomic<bool> busy_{false};
+  bool stop_ = false;
+};
+
+// host entry-point calls in flight (the pipelined, pool-assisted form is for
+// few callers; many concurrent callers are better served one piece each)
+std::atomic<int> g_host_calls{0};
 }  // namespace
+
+void host_parallel_for(int n, const std::function<void(int)> &fn) { HostPool::get().parallel_for(n, fn); }
 
 int set_error(int code, const char *fmt, ...) {
   char buf[512];
@@ -299,6 +395,7 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
       (void)hipStreamSynchronize(s->stream);
       (void)hipStreamDestroy(s->stream);
     }
+    for (hipEvent_t ev : s->events) (void)hipEventDestroy(ev);
     if (s->h) (void)hipHostFree(s->h);
     if (s->d) (void)hipFree(s->d);
     delete s;
@@ -974,34 +1071,74 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   int rc = default_ctx(&ctx);
   if (rc) return rc;
   const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;  // keep chunks 16-B aligned in staging
-  const int nchunks = k + rows + ncopy;
+  const int nout = rows + ncopy;
+  const int nchunks = k + nout;
   Slot *slot = nullptr;
   rc = acquire_slot(ctx, static_cast<size_t>(stride) * nchunks, &slot);
   if (rc) return rc;
-  for (int j = 0; j < k; j++) std::memcpy(slot->h + j * stride, data[j], static_cast<size_t>(len));
-  hipError_t e = hipMemcpyAsync(slot->d, slot->h, static_cast<size_t>(stride) * k, hipMemcpyHostToDevice, slot->stream);
-  if (e != hipSuccess) {
-    release_slot(ctx, slot);
-    return hip_err(e, "H2D");
+  // Pipelined in column pieces: the pool copies piece p of every input into
+  // pinned staging while the copy engine and the kernel work on piece p-1;
+  // outputs come back per piece.  Staging layout [k inputs][rows outputs]
+  // [ncopy pass-through outputs], each chunk at a 16-byte stride.
+  struct InFlight {
+    int n;
+    InFlight() : n(g_host_calls.fetch_add(1) + 1) {}
+    ~InFlight() { g_host_calls.fetch_sub(1); }
+  } inflight;
+  const int64_t piece = (len >= 2 * kHostPiece && inflight.n <= 2) ? kHostPiece : stride;
+  const int npieces = static_cast<int>((len + piece - 1) / piece);
+  while (static_cast<int>(slot->events.size()) < npieces) {
+    hipEvent_t ev;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      release_slot(ctx, slot);
+      return hip_err(e, "hipEventCreate");
+    }
+    slot->events.push_back(ev);
   }
-  // staging layout: [k inputs][rows outputs][ncopy pass-through outputs]
   std::vector<int32_t> dst(std::max(rows, 1)), cpy(k, -1);
   for (int r = 0; r < rows; r++) dst[r] = k + r;
   for (int j = 0; j < k; j++)
     if (copy_idx && copy_idx[j] >= 0) cpy[j] = k + rows + copy_idx[j];
-  rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d, nullptr, stride, 0, slot->d, dst.data(), stride, 0,
-                        ncopy ? cpy.data() : nullptr, len, 1, slot->stream);
-  if (rc == NXEC_OK) {
-    e = hipMemcpyAsync(slot->h + stride * k, slot->d + stride * k, static_cast<size_t>(stride) * (rows + ncopy),
-                       hipMemcpyDeviceToHost, slot->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(slot->stream);
-    if (e != hipSuccess) rc = hip_err(e, "D2H/sync");
+  HostPool &pool = HostPool::get();
+  for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
+    const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
+    pool.parallel_for(k, [&](int j) { std::memcpy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
+    hipError_t e = hipMemcpy2DAsync(slot->d + off, stride, slot->h + off, stride, static_cast<size_t>(pl), k,
+                                    hipMemcpyHostToDevice, slot->stream);
+    if (e != hipSuccess) {
+      rc = hip_err(e, "H2D");
+      break;
+    }
+    rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d + off, nullptr, stride, 0, slot->d + off, dst.data(), stride, 0,
+                          ncopy ? cpy.data() : nullptr, pl, 1, slot->stream);
+    if (rc) break;
+    e = hipMemcpy2DAsync(slot->h + stride * k + off, stride, slot->d + stride * k + off, stride, static_cast<size_t>(pl),
+                         nout, hipMemcpyDeviceToHost, slot->stream);
+    if (e == hipSuccess) e = hipEventRecord(slot->events[pc], slot->stream);
+    if (e != hipSuccess) rc = hip_err(e, "D2H");
   }
   if (rc == NXEC_OK) {
-    for (int r = 0; r < rows; r++) std::memcpy(coding[r], slot->h + (k + r) * stride, static_cast<size_t>(len));
-    for (int j = 0; j < k; j++)
-      if (copy_idx && copy_idx[j] >= 0)
-        std::memcpy(copy_out[copy_idx[j]], slot->h + (k + rows + copy_idx[j]) * stride, static_cast<size_t>(len));
+    for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
+      const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
+      hipError_t e = hipEventSynchronize(slot->events[pc]);
+      if (e != hipSuccess) {
+        rc = hip_err(e, "piece sync");
+        break;
+      }
+      pool.parallel_for(nout, [&](int o) {
+        unsigned char *to = nullptr;
+        if (o < rows) {
+          to = coding[o];
+        } else {
+          for (int j = 0; j < k; j++)
+            if (copy_idx && copy_idx[j] == o - rows) to = copy_out[o - rows];
+        }
+        if (to) std::memcpy(to + off, slot->h + (k + o) * stride + off, static_cast<size_t>(pl));
+      });
+    }
+  } else {
+    (void)hipStreamSynchronize(slot->stream);
   }
   release_slot(ctx, slot);
   return rc;

@@ -702,3 +702,43 @@ def test_rs16_4_full_batch_mixed(gpu_ctx, cs):
         want = oracle.matmul(nxec.gen_rs_matrix(n, k)[k:], list(h[:k]))
         assert all(np.array_equal(h[k + r], want[r]) for r in range(n - k)), s
     buf.free()
+
+
+@pytest.mark.parametrize("cs,threads", [((1 << 20) + 5, 1), (600000, 1), ((1 << 20) + 3, 2), ((1 << 20) + 3, 6)])
+def test_encode_host_ex_pipelined(gpu_ctx, cs, threads):
+    """The host entry point (RSCode / CodingUtils / ec_encode_data) copies in
+    column pieces pipelined with the DMA and kernel when few callers are in
+    flight (one piece each otherwise): parity rows and pass-through copies
+    (the unit rows of a full-output decode) are bit-exact either way."""
+    import threading
+    n, k = 14, 10
+    rows = 4
+    enc = nxec.gen_rs_matrix(n, k)[k:]
+    lib = nxec.lib
+    errs = []
+
+    def work(t):
+        try:
+            data = fill_bytes(k * cs, 300 + t).reshape(k, cs)
+            outs = np.zeros((rows, cs), dtype=np.uint8)
+            copies = np.zeros((2, cs), dtype=np.uint8)
+            copy_idx = np.full(k, -1, dtype=np.int32)
+            copy_idx[3], copy_idx[7] = 0, 1
+            c = np.ascontiguousarray(enc, dtype=np.uint8)
+            inp = (C.c_void_p * k)(*[data[j].ctypes.data for j in range(k)])
+            outp = (C.c_void_p * rows)(*[outs[r].ctypes.data for r in range(rows)])
+            cpp = (C.c_void_p * 2)(copies[0].ctypes.data, copies[1].ctypes.data)
+            for _ in range(3):
+                rc = lib.nxec_encode_host_ex(cs, k, rows, C.c_void_p(c.ctypes.data), inp, outp,
+                                             C.c_void_p(copy_idx.ctypes.data), cpp)
+                assert rc == 0, rc
+            want = oracle.matmul(enc, list(data))
+            assert all(np.array_equal(outs[r], want[r]) for r in range(rows)), t
+            assert np.array_equal(copies[0], data[3]) and np.array_equal(copies[1], data[7]), t
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not errs, errs
