@@ -796,12 +796,14 @@ int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
   if (b.reqs.empty()) return NXEC_OK;
   NXEC_HIP(hipStreamSynchronize(b.slot->stream));
   const nxec_agent_req &r0 = reqs[b.reqs[0]];
-  for (size_t i = 0; i < b.reqs.size(); i++) {
+  const int no = r0.noutputs;
+  HostPool::get().parallel_for(static_cast<int>(b.reqs.size()) * no, [&](int item) {  // scatter the outputs
+    const size_t i = static_cast<size_t>(item / no);
+    const int o = item % no;
     const nxec_agent_req &r = reqs[b.reqs[i]];
-    for (int o = 0; o < r0.noutputs; o++)
-      std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * r0.noutputs + o) * b.stride, cs);
-    if (r.md5) std::memcpy(r.md5, b.slot->h + b.md5_off + i * r0.noutputs * 16, size_t(r0.noutputs) * 16);
-  }
+    std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * no + o) * b.stride, cs);
+    if (o == 0 && r.md5) std::memcpy(r.md5, b.slot->h + b.md5_off + i * no * 16, size_t(no) * 16);
+  });
   b.reqs.clear();
   return NXEC_OK;
 }
@@ -856,11 +858,12 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
       b.stride = stride;
       b.out_off = in_bytes;
       b.md5_off = in_bytes + size_t(nb) * no * stride;
-      for (int64_t i = 0; i < nb; i++) {  // gather the request's chunks into pinned staging
-        const nxec_agent_req &r = reqs[ids[first + i]];
-        for (int j = 0; j < ni; j++) std::memcpy(b.slot->h + (i * ni + j) * stride, r.inputs[j], chunk_size);
-        b.reqs.push_back(ids[first + i]);
-      }
+      HostPool::get().parallel_for(static_cast<int>(nb) * ni, [&](int item) {  // gather into pinned staging
+        const int64_t i = item / ni;
+        const int j = item % ni;
+        std::memcpy(b.slot->h + (i * ni + j) * stride, reqs[ids[first + i]].inputs[j], chunk_size);
+      });
+      for (int64_t i = 0; i < nb; i++) b.reqs.push_back(ids[first + i]);
       hipStream_t st = b.slot->stream;
       uint8_t *d_in = b.slot->d, *d_out = b.slot->d + b.out_off, *d_md5 = b.slot->d + b.md5_off;
       bool any_md5 = false;
