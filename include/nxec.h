@@ -299,6 +299,28 @@ typedef struct nxec_agent_req {
 int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
                             int64_t batch_bytes);
 
+/* ---- Multi-GPU group in one process: one context per device,
+ * a batch's stripes split into contiguous ranges (sizes differ by at most one),
+ * one host thread per device; no collective, no peer traffic.  Calls are
+ * synchronous.  A device may appear twice (two contexts on one GPU). */
+typedef struct nxec_group nxec_group_t;
+int nxec_group_create(const int *devices, int ndevices, nxec_group_t **out);
+void nxec_group_destroy(nxec_group_t *g);
+int nxec_group_size(const nxec_group_t *g);
+nxec_ctx_t *nxec_group_ctx(nxec_group_t *g, int i);
+/* stripes [first, first+count) of `nstripes` belong to part `part` of `nparts` */
+int nxec_group_shard(int64_t nstripes, int nparts, int part, int64_t *first, int64_t *count);
+/* nxec_rs_encode_host_batch over the group: device i encodes its shard of the
+ * host [nstripes][k][len] data into host [nstripes][n-k][len] parity */
+int nxec_group_rs_encode_host_batch(nxec_group_t *g, int n, int k, const unsigned char *h_data,
+                                    unsigned char *h_parity, int64_t len, int64_t nstripes, int64_t batch_stripes);
+/* device-resident shards: d_stripes[i] / nstripes[i] live on the group's device i */
+int nxec_group_rs_encode_stripes(nxec_group_t *g, int n, int k, unsigned char *const *d_stripes, int64_t chunk_stride,
+                                 int64_t stripe_stride, int64_t len, const int64_t *nstripes);
+int nxec_group_rs_recover_stripes(nxec_group_t *g, int n, int k, const int32_t *failed, int nfailed,
+                                  unsigned char *const *d_stripes, int64_t chunk_stride, int64_t stripe_stride,
+                                  int64_t len, const int64_t *nstripes);
+
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU
  *    framework can drive section 3.  Thin wrappers over the HIP runtime.

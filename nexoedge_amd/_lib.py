@@ -96,6 +96,14 @@ _PROTOS = {
     "nxec_fill_random": (C.c_int, [vp, C.c_size_t, C.c_uint64, vp]),
     "nxec_checksum": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), vp]),
     "nxec_describe_launch": (C.c_int, [vp, C.c_int, C.c_int, i64, i64, C.c_char_p, C.c_int]),
+    "nxec_group_create": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
+    "nxec_group_destroy": (None, [vp]),
+    "nxec_group_size": (C.c_int, [vp]),
+    "nxec_group_ctx": (vp, [vp, C.c_int]),
+    "nxec_group_shard": (C.c_int, [i64, C.c_int, C.c_int, C.POINTER(i64), C.POINTER(i64)]),
+    "nxec_group_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
+    "nxec_group_rs_encode_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, vp]),
+    "nxec_group_rs_recover_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, vp]),
 }
 
 class AgentReq(C.Structure):

@@ -388,8 +388,57 @@ class Context:
             self.ptr = 0
 
 
+class Group:
+    """nxec_group_t: one context per device, stripes sharded in contiguous
+    ranges, one host thread per device (no collectives)."""
+
+    def __init__(self, devices: Sequence[int]):
+        d = np.ascontiguousarray(list(devices), dtype=np.int32)
+        p = C.c_void_p()
+        check(lib.nxec_group_create(C.c_void_p(d.ctypes.data), len(d), C.byref(p)), "nxec_group_create")
+        self.ptr = p.value
+        self.devices = [int(x) for x in d]
+
+    def __len__(self) -> int:
+        return int(lib.nxec_group_size(C.c_void_p(self.ptr)))
+
+    @staticmethod
+    def shard(nstripes: int, nparts: int, part: int):
+        """(first, count) of part `part` (nxec_group_shard)."""
+        f, c = C.c_int64(), C.c_int64()
+        check(lib.nxec_group_shard(nstripes, nparts, part, C.byref(f), C.byref(c)), "nxec_group_shard")
+        return int(f.value), int(c.value)
+
+    def rs_encode_host_batch(self, n: int, k: int, h_data: int, h_parity: int, length: int, nstripes: int,
+                             batch_stripes: int = 0) -> None:
+        check(lib.nxec_group_rs_encode_host_batch(C.c_void_p(self.ptr), n, k, C.c_void_p(int(h_data)),
+                                                  C.c_void_p(int(h_parity)), length, nstripes, batch_stripes),
+              "nxec_group_rs_encode_host_batch")
+
+    def rs_encode(self, n: int, k: int, stripes: Sequence[int], chunk_stride: int, stripe_stride: int, length: int,
+                  nstripes: Sequence[int]) -> None:
+        ptrs = (C.c_void_p * len(stripes))(*[int(x) for x in stripes])
+        ns = np.ascontiguousarray(list(nstripes), dtype=np.int64)
+        check(lib.nxec_group_rs_encode_stripes(C.c_void_p(self.ptr), n, k, ptrs, chunk_stride, stripe_stride, length,
+                                               C.c_void_p(ns.ctypes.data)), "nxec_group_rs_encode_stripes")
+
+    def rs_recover(self, n: int, k: int, failed: Sequence[int], stripes: Sequence[int], chunk_stride: int,
+                   stripe_stride: int, length: int, nstripes: Sequence[int]) -> None:
+        f = np.ascontiguousarray(list(failed), dtype=np.int32)
+        ptrs = (C.c_void_p * len(stripes))(*[int(x) for x in stripes])
+        ns = np.ascontiguousarray(list(nstripes), dtype=np.int64)
+        check(lib.nxec_group_rs_recover_stripes(C.c_void_p(self.ptr), n, k, C.c_void_p(f.ctypes.data), len(f), ptrs,
+                                                chunk_stride, stripe_stride, length, C.c_void_p(ns.ctypes.data)),
+              "nxec_group_rs_recover_stripes")
+
+    def close(self) -> None:
+        if self.ptr:
+            lib.nxec_group_destroy(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+
 __all__ = [
-    "NxecError", "gf_mul", "gf_inv", "gen_rs_matrix", "invert_matrix", "init_tables", "rs_plan", "decode_matrix",
+    "Group", "NxecError", "gf_mul", "gf_inv", "gen_rs_matrix", "invert_matrix", "init_tables", "rs_plan", "decode_matrix",
     "encode_host", "ec_encode_data", "car_plan", "device_count", "device_info", "device_sync", "DeviceBuffer", "PinnedBuffer",
     "Event", "Context",
 ]

@@ -51,6 +51,34 @@ def free_port():
     return p
 
 
+def test_group_shard_matches_rank_sharding():
+    """The in-process multi-GPU group (nxec_group_*) splits stripes exactly like
+    the one-process-per-GPU ranks do, so both deployments code the same ranges."""
+    from nexoedge_amd import nxec
+
+    for total in (0, 1, 7, 4096, 4097, 10**6 + 3):
+        for world in (1, 2, 3, 8):
+            for r in range(world):
+                lo, hi = shard_range(total, r, world)
+                assert nxec.Group.shard(total, world, r) == (lo, hi - lo)
+
+
+def test_group_without_device_fails_loudly():
+    import pytest
+
+    from nexoedge_amd import nxec
+
+    try:
+        import torch
+
+        if torch.cuda.device_count() > 0:
+            pytest.skip("a device is present")
+    except ImportError:
+        pass
+    with pytest.raises(nxec.NxecError):
+        nxec.Group([0, 0])
+
+
 def test_gloo_world2_reduction(tmp_path):
     script = tmp_path / "w.py"
     script.write_text(WORKER.format(root=ROOT))

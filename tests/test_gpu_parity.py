@@ -742,3 +742,48 @@ def test_encode_host_ex_pipelined(gpu_ctx, cs, threads):
     [x.start() for x in th]
     [x.join() for x in th]
     assert not errs, errs
+
+
+def test_group_two_contexts_host_and_device(gpu_ctx):
+    """nxec_group over two contexts on device 0 (the only one here): the
+    host-batch encode shards stripes across both, and device-resident shards
+    encode + recover independently; bit-exact vs the oracle."""
+    n, k, cs, ns = 14, 10, 65536 + 16, 7
+    p = n - k
+    g = nxec.Group([0, 0])
+    try:
+        assert len(g) == 2
+        hd = nxec.PinnedBuffer(ns * k * cs)
+        hp = nxec.PinnedBuffer(ns * p * cs)
+        data = [fill_bytes(k * cs, 5100 + s) for s in range(ns)]
+        hd.array[:] = np.concatenate(data)
+        g.rs_encode_host_batch(n, k, hd.ptr, hp.ptr, cs, ns, 2)
+        enc = nxec.gen_rs_matrix(n, k)[k:]
+        par = hp.array.reshape(ns, p, cs)
+        for s in range(ns):
+            want = oracle.matmul(enc, list(data[s].reshape(k, cs)))
+            assert all(np.array_equal(par[s, r], want[r]) for r in range(p)), s
+        hd.free()
+        hp.free()
+        # device-resident shards, one buffer per group member
+        counts = [g.shard(ns, 2, i)[1] for i in range(2)]
+        bufs, hosts = [], []
+        for i, c in enumerate(counts):
+            b, h = stripe_buffer(n, k, cs, cs, data[:c] if i == 0 else data[counts[0]:])
+            bufs.append(b)
+            hosts.append(h)
+        g.rs_encode(n, k, [b.ptr for b in bufs], cs, n * cs, cs, counts)
+        sums = [b.checksum() for b in bufs]
+        for b, c in zip(bufs, counts):
+            erase_chunks(gpu_ctx, b, n, cs, c, [1, 4, 11, 13])
+        gpu_ctx.sync()
+        g.rs_recover(n, k, [1, 4, 11, 13], [b.ptr for b in bufs], cs, n * cs, cs, counts)
+        assert [b.checksum() for b in bufs] == sums
+        got = bufs[1].download().reshape(counts[1], n, cs)
+        for s in range(counts[1]):
+            want = oracle.matmul(enc, list(data[counts[0] + s].reshape(k, cs)))
+            assert all(np.array_equal(got[s, k + r], want[r]) for r in range(p)), s
+        for b in bufs:
+            b.free()
+    finally:
+        g.close()
