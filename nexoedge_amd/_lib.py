@@ -106,6 +106,7 @@ _PROTOS = {
     "nxec_group_rs_recover_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, vp]),
 }
 
+
 class AgentReq(C.Structure):
     """struct nxec_agent_req of include/nxec.h"""
     _fields_ = [("ninputs", C.c_int), ("noutputs", C.c_int), ("matrix", vp), ("inputs", vp), ("outputs", vp),

@@ -47,7 +47,7 @@ constexpr int kLdsBytes = 160 * 1024;
 // next-tile prefetch doubles the source registers (4*K VGPRs); beyond these k
 // the 128-VGPR budget of a 1024-thread workgroup would spill
 constexpr int kPrefetchMaxK = 10;
-constexpr int kPrefetchMaxKCopy = 8;
+constexpr int kPrefetchMaxKCopy = 8;  // k = 10 with copies fits (123 VGPRs) but measured 6-8% slower (full-output decode)
 constexpr int kPermPrefetchMaxK = 4;
 constexpr int kPermMaxK = 13;  // beyond this the single-row VALU kernel would spill (128-VGPR budget)
 
