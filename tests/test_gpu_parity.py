@@ -547,7 +547,7 @@ def test_survey_named_encode_entry_points(gpu_ctx):
 
 
 @pytest.mark.parametrize("misalign,n,k,M", [(0, 9, 6, 4096), (3, 9, 6, 4096), (0, 9, 6, 1000), (0, 14, 10, 65536),
-                                             (5, 14, 10, 16400), (0, 24, 20, 4096)])
+                                             (5, 14, 10, 16400), (0, 24, 20, 4096), (0, 6, 6, 4096)])
 def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
     """Many objects per call (full stripes in one gather launch, last stripes in
     one ragged work-queue launch -- the list kernel for k > 19 --, MD5 of every
@@ -569,7 +569,7 @@ def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
     tail = nxec.DeviceBuffer(max(tail_bytes, 16))
     md5 = nxec.DeviceBuffer(total * n * 16)
     gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
-    gp = par.download().reshape(total, p, M)
+    gp = par.download(total * p * M).reshape(total, p, M)
     gm = md5.download().reshape(total, n, 16)
     gt = tail.download()
     g, toff = 0, 0
@@ -587,10 +587,10 @@ def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
             assert not got[:, cl:].any(), i
             toff += k * cls
         ob = up(host[o:o + L])
-        op, ot, om = nxec.DeviceBuffer(ns * p * M), nxec.DeviceBuffer(k * M), nxec.DeviceBuffer(ns * n * 16)
+        op, ot, om = nxec.DeviceBuffer(max(ns * p * M, 1)), nxec.DeviceBuffer(k * M), nxec.DeviceBuffer(ns * n * 16)
         gpu_ctx.encode_object(n, k, ob.ptr, L, M, op.ptr, ot.ptr, om.ptr)
         gpu_ctx.sync()
-        wp = op.download().reshape(ns, p, M)
+        wp = op.download(ns * p * M).reshape(ns, p, M)
         for s in range(ns):
             cs = M if s < nf else cl
             assert np.array_equal(gp[g + s, :, :cs], wp[s, :, :cs]), (i, s)
