@@ -165,9 +165,10 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
                            int64_t nstripes, void *stream);
 
 /* Host-resident batch encode (the proxy write path): h_data [s][k][len] in,
- * h_parity [s][n-k][len] out, both host memory (pinned/registered memory is
- * DMA'd directly; pageable memory is staged).  Double-buffered H2D -> kernel
- * -> D2H over `batch_stripes` stripes per step.  Synchronous. */
+ * h_parity [s][n-k][len] out, both host memory.  When both are pinned or
+ * registered (device-mapped) the kernel reads and writes them over PCIe
+ * directly (zero copy; NXEC_HOST_DIRECT=0 disables); otherwise double-buffered
+ * H2D -> kernel -> D2H over `batch_stripes` stripes per step.  Synchronous. */
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data,
                               unsigned char *h_parity, int64_t len, int64_t nstripes, int64_t batch_stripes);
 

@@ -895,6 +895,21 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
   return rc;
 }
 
+// Device address of pinned / registered host memory (the kernel can read and
+// write it over PCIe), or nullptr for pageable memory.
+namespace {
+void *host_device_view(const void *h) {
+  const char *env = std::getenv("NXEC_HOST_DIRECT");
+  if (env && env[0] == '0') return nullptr;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, h) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+}  // namespace
+
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,
                               int64_t len, int64_t nstripes, int64_t batch_stripes) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
@@ -904,6 +919,23 @@ int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
   const int p = n - k;
+  // Pinned / registered buffers: zero copy.  The coding kernel reads the data
+  // and writes the parity over PCIe itself; its ~1 KiB requests from every CU
+  // keep more of the link busy than the copy engines do (RS(10,4) 1 MiB,
+  // 512 stripes: 71.6 vs 48.7 GiB/s of (k+p)*cs, tools/zero_copy_probe.py).
+  {
+    const unsigned char *dd = static_cast<const unsigned char *>(host_device_view(h_data));
+    unsigned char *dp = static_cast<unsigned char *>(host_device_view(h_parity));
+    if (dd && dp) {
+      std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+      nxec_gf_gen_rs_matrix(enc.data(), n, k);
+      hipStream_t st = pick_stream(ctx, nullptr);
+      rc = nxec_stripes_mul(ctx, p, k, enc.data() + static_cast<size_t>(k) * k, dd, nullptr, len, k * len, dp, nullptr,
+                            len, p * len, nullptr, len, nstripes, st);
+      if (rc) return rc;
+      return hip_check(hipStreamSynchronize(st), "encode_host_batch (direct) sync");
+    }
+  }
   if (batch_stripes <= 0) batch_stripes = std::max<int64_t>(1, (int64_t(256) << 20) / (len * n));
   batch_stripes = std::min(batch_stripes, nstripes);
   std::vector<uint8_t> enc(static_cast<size_t>(n) * k);

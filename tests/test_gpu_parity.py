@@ -787,3 +787,33 @@ def test_group_two_contexts_host_and_device(gpu_ctx):
             b.free()
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("mode", ["pinned-direct", "pinned-dma", "pageable"])
+def test_rs_encode_host_batch_paths(gpu_ctx, monkeypatch, mode):
+    """Host-resident batch encode: zero copy over PCIe for pinned buffers, the
+    double-buffered DMA path when disabled (NXEC_HOST_DIRECT=0) or for pageable
+    buffers; parity bit-exact vs the oracle either way."""
+    n, k, cs, ns = 14, 10, 65536 + 48, 9
+    p = n - k
+    if mode == "pinned-dma":
+        monkeypatch.setenv("NXEC_HOST_DIRECT", "0")
+    data = [fill_bytes(k * cs, 6200 + s) for s in range(ns)]
+    if mode == "pageable":
+        hd = np.concatenate(data)
+        hp = np.zeros(ns * p * cs, dtype=np.uint8)
+        dptr, pptr, parr = hd.ctypes.data, hp.ctypes.data, hp
+    else:
+        hdb, hpb = nxec.PinnedBuffer(ns * k * cs), nxec.PinnedBuffer(ns * p * cs)
+        hdb.array[:] = np.concatenate(data)
+        hpb.array[:] = 0
+        dptr, pptr, parr = hdb.ptr, hpb.ptr, hpb.array
+    gpu_ctx.rs_encode_host_batch(n, k, dptr, pptr, cs, ns, 4)
+    enc = nxec.gen_rs_matrix(n, k)[k:]
+    par = parr.reshape(ns, p, cs)
+    for s in range(ns):
+        want = oracle.matmul(enc, list(data[s].reshape(k, cs)))
+        assert all(np.array_equal(par[s, r], want[r]) for r in range(p)), s
+    if mode != "pageable":
+        hdb.free()
+        hpb.free()
