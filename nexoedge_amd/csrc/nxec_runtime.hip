@@ -122,6 +122,20 @@ class HostPool {
   bool stop_ = false;
 };
 
+// Device address of pinned / registered host memory (kernels read and write
+// it over PCIe: zero copy), or nullptr for pageable memory or when
+// NXEC_HOST_DIRECT=0.
+void *host_device_view(const void *h) {
+  const char *env = std::getenv("NXEC_HOST_DIRECT");
+  if (env && env[0] == '0') return nullptr;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, h) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+
 // host entry-point calls in flight (the pipelined, pool-assisted form is for
 // few callers; many concurrent callers are better served one piece each)
 std::atomic<int> g_host_calls{0};
@@ -895,21 +909,6 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
   return rc;
 }
 
-// Device address of pinned / registered host memory (the kernel can read and
-// write it over PCIe), or nullptr for pageable memory.
-namespace {
-void *host_device_view(const void *h) {
-  const char *env = std::getenv("NXEC_HOST_DIRECT");
-  if (env && env[0] == '0') return nullptr;
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, h) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
-}
-}  // namespace
-
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,
                               int64_t len, int64_t nstripes, int64_t batch_stripes) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
@@ -1136,20 +1135,30 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   for (int j = 0; j < k; j++)
     if (copy_idx && copy_idx[j] >= 0) cpy[j] = k + rows + copy_idx[j];
   HostPool &pool = HostPool::get();
+  // Few callers: zero copy, the kernel works on the pinned staging itself over
+  // PCIe (no copy-engine round trip: 1 caller 25.8 -> 33.6 GiB/s).  Many
+  // callers: H2D -> kernel -> D2H per piece, whose copy engines share the link
+  // better (4 callers 69.8 vs 52.0 GiB/s zero copy; profiles/r01_dropin*.jsonl).
+  uint8_t *hv = inflight.n <= 2 ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
   for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
     const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
     pool.parallel_for(k, [&](int j) { std::memcpy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
-    hipError_t e = hipMemcpy2DAsync(slot->d + off, stride, slot->h + off, stride, static_cast<size_t>(pl), k,
-                                    hipMemcpyHostToDevice, slot->stream);
-    if (e != hipSuccess) {
-      rc = hip_err(e, "H2D");
-      break;
+    hipError_t e = hipSuccess;
+    uint8_t *base = hv ? hv : slot->d;
+    if (!hv) {
+      e = hipMemcpy2DAsync(slot->d + off, stride, slot->h + off, stride, static_cast<size_t>(pl), k,
+                           hipMemcpyHostToDevice, slot->stream);
+      if (e != hipSuccess) {
+        rc = hip_err(e, "H2D");
+        break;
+      }
     }
-    rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d + off, nullptr, stride, 0, slot->d + off, dst.data(), stride, 0,
+    rc = nxec_stripes_mul(ctx, rows, k, coeffs, base + off, nullptr, stride, 0, base + off, dst.data(), stride, 0,
                           ncopy ? cpy.data() : nullptr, pl, 1, slot->stream);
     if (rc) break;
-    e = hipMemcpy2DAsync(slot->h + stride * k + off, stride, slot->d + stride * k + off, stride, static_cast<size_t>(pl),
-                         nout, hipMemcpyDeviceToHost, slot->stream);
+    if (!hv)
+      e = hipMemcpy2DAsync(slot->h + stride * k + off, stride, slot->d + stride * k + off, stride,
+                           static_cast<size_t>(pl), nout, hipMemcpyDeviceToHost, slot->stream);
     if (e == hipSuccess) e = hipEventRecord(slot->events[pc], slot->stream);
     if (e != hipSuccess) rc = hip_err(e, "D2H");
   }
