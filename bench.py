@@ -506,7 +506,41 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     hd.free()
     hp.free()
     hm.free()
+    out["read_frames_decode_GiB_s_user_data"] = round(read_from_frames(ctx, n, k, cs, min(ns, 128)), 2)
     return out
+
+
+def read_from_frames(ctx, n, k, cs, ns):
+    """The proxy read path on received chunk frames (pageable message buffers,
+    one per chunk): gather the k surviving chunks of every stripe into the
+    device batch, full-output decode of 4 erasures, scatter the k data chunks
+    into per-chunk host frames.  User-data GiB/s."""
+    import numpy as np
+
+    failed = list(range(k - (n - k), k))  # worst case: n-k data chunks lost
+    alive = [c for c in range(n) if c not in failed]
+    rx = np.random.default_rng(2).integers(0, 256, size=ns * k * cs, dtype=np.uint8)
+    tx = np.empty(ns * k * cs, dtype=np.uint8)
+    st = nxec.DeviceBuffer(ns * n * cs)
+    dec = nxec.DeviceBuffer(ns * k * cs)
+    rx_frames = {c: [rx.ctypes.data + (s * k + i) * cs for s in range(ns)] for i, c in enumerate(alive)}
+    tx_frames = [tx.ctypes.data + i * cs for i in range(ns * k)]
+
+    def once():
+        for c in alive:
+            ctx.gather_chunks(rx_frames[c], cs, st.ptr + c * cs, n * cs)
+        ctx.rs_decode(n, k, failed, st.ptr, cs, n * cs, dec.ptr, cs, k * cs, cs, ns)
+        ctx.scatter_chunks(dec.ptr, cs, tx_frames, cs)
+
+    once()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    dt = (time.perf_counter() - t0) / reps
+    st.free()
+    dec.free()
+    return ns * k * cs / dt / GIB
 
 
 def cpu_write_path(args, n, k, cs):

@@ -214,6 +214,16 @@ int nxec_rs_car_repair_stripes(nxec_ctx_t *ctx, int n, int k, int failed, const 
 int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
                     int nchunks, int64_t len, int64_t nstripes, unsigned char *d_digests, void *stream);
 
+/* Chunk::verifyMD5 over a batch: the read path's check of every fetched chunk
+ * (chunk_manager.cc:1553-1555) and the agent's VRF_CHUNK_REQ scan
+ * (ContainerManager::verifyChunks, container_manager.cc:187-207).  Hashes like
+ * nxec_md5_chunks and compares with d_expected (same [s][c][16] layout):
+ * d_ok[s*nchunks + c] = 1 if equal, 0 if not; *d_nbad (device, optional, not
+ * reset) += the number of mismatches. */
+int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
+                           int nchunks, int64_t len, int64_t nstripes, const unsigned char *d_expected,
+                           unsigned char *d_ok, unsigned long long *d_nbad, void *stream);
+
 /* ---- Object-level batched entry (ChunkManager write/read of a
  * whole object in one call instead of the per-stripe loop of
  * proxy_file_ops.cc:557-666 / chunk_manager.cc:99,787).
@@ -299,6 +309,24 @@ typedef struct nxec_agent_req {
 
 int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
                             int64_t batch_bytes);
+
+/* ---- Chunk frames <-> device batch (the in-scope part of the
+ * wire format).  IO::getChunkEventMessage mallocs and memcpys every received
+ * chunk frame (common/io.cc:209-216) and sendChunkEventMessage sends one frame
+ * per chunk (:334-336); these move such frames straight between their message
+ * buffers and a strided device batch, so received chunks feed
+ * nxec_rs_decode_stripes / nxec_decode_object and encoded chunks go out
+ * without a per-chunk malloc.
+ * nxec_gather_chunks:  h_chunks[i] (len bytes) -> d_dst + i*dst_stride
+ * nxec_scatter_chunks: d_src + i*src_stride    -> h_chunks[i]
+ * Any alignment; pinned / registered frames of >= 8 MiB are DMA'd directly, others
+ * go through the context's pinned slots (host pool packs piece p while the copy
+ * engine moves piece p-1).  Synchronous: the frames may be reused or read on
+ * return.  `stream` orders the device side (NULL = context stream). */
+int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, int64_t nchunks, int64_t len,
+                       unsigned char *d_dst, int64_t dst_stride, void *stream);
+int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks, int64_t len,
+                        unsigned char *const *h_chunks, void *stream);
 
 /* ---- Multi-GPU group in one process: one context per device,
  * a batch's stripes split into contiguous ranges (sizes differ by at most one),

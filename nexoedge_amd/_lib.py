@@ -62,6 +62,7 @@ _PROTOS = {
         [vp, C.c_int, C.c_int, C.c_int, vp, vp, C.c_int, vp, i64, i64, vp, i64, i64, i64, i64, vp],
     ),
     "nxec_md5_chunks": (C.c_int, [vp, vp, i64, i64, C.c_int, i64, i64, vp, vp]),
+    "nxec_md5_verify_chunks": (C.c_int, [vp, vp, i64, i64, C.c_int, i64, i64, vp, vp, vp, vp]),
     "nxec_object_layout": (C.c_int, [C.c_int, C.c_int, i64, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, vp, vp]),
     "nxec_encode_object_host": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, i64]),
@@ -70,7 +71,9 @@ _PROTOS = {
     "nxec_decode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp]),
     "nxec_agent_encode_batch": (C.c_int, [vp, vp, C.c_int, i64, i64]),
     "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
-    "nxec_rs_plan": (C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
+    "nxec_gather_chunks": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
+    "nxec_scatter_chunks": (C.c_int, [vp, vp, i64, i64, i64, vp, vp]),
+    "nxec_rs_plan":(C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
     "nxec_rs_decode_matrix": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp]),
     "nxec_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "nxec_set_device": (C.c_int, [C.c_int]),

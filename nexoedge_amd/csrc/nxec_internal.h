@@ -85,7 +85,10 @@ struct Md5Region {
   int64_t dig_stripe_stride;
   int nchunks;
 };
-int launch_md5(const Md5Region *regions, int nregions, void *stream);
+// verify mode (ok != nullptr, one region): `digests` holds the expected
+// digests; ok[s*nchunks + i] = match, *nbad += mismatches (nbad optional)
+int launch_md5(const Md5Region *regions, int nregions, void *stream, uint8_t *ok = nullptr,
+               unsigned long long *nbad = nullptr);
 int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
 
 // Variable-length batch (many objects per call): stripe s has its own chunk

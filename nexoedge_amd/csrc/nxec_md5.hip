@@ -211,6 +211,10 @@ struct Md5Args {
   int nregions;
   const Md5Item *items;  // list mode (items != nullptr): lane c hashes items[c]
   int64_t nitems;
+  // verify mode (ok != nullptr): the region's digests are the expected ones,
+  // lane c writes ok[c] = digest matches, and counts mismatches into *nbad
+  uint8_t *ok;
+  unsigned long long *nbad;
 };
 
 // one lane per chunk over the concatenated regions
@@ -285,6 +289,14 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
     }
     md5_block(h, m);
   }
+  if (args.ok) {  // Chunk::verifyMD5: recompute and compare (chunk_manager.cc:1555, container_manager.cc:187-207)
+    bool same = true;
+#pragma unroll
+    for (int i = 0; i < 16; i++) same &= out[i] == static_cast<uint8_t>(h[i / 4] >> (8 * (i % 4)));
+    args.ok[c] = same ? 1 : 0;
+    if (!same && args.nbad) atomicAdd(args.nbad, 1ull);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(h[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
 }
@@ -318,8 +330,10 @@ Md5Kernel md5_kernel() {
 
 }  // namespace
 
-int launch_md5(const Md5Region *regions, int nregions, void *stream) {
+int launch_md5(const Md5Region *regions, int nregions, void *stream, uint8_t *ok, unsigned long long *nbad) {
   Md5Args args{};
+  args.ok = ok;
+  args.nbad = nbad;
   int64_t total = 0;
   int nr = 0;
   for (int i = 0; i < nregions && i < kMaxMd5Regions; i++) {

@@ -538,6 +538,20 @@ int nxec_md5_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_
   return launch_md5(&r, 1, pick_stream(ctx, stream));
 }
 
+int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t chunk_stride, int64_t stripe_stride,
+                           int nchunks, int64_t len, int64_t nstripes, const unsigned char *d_expected,
+                           unsigned char *d_ok, unsigned long long *d_nbad, void *stream) {
+  if (!ctx || nchunks < 0 || len < 0 || nstripes < 0 ||
+      ((nchunks > 0 && nstripes > 0) && (!d_base || !d_expected || !d_ok)))
+    return set_error(NXEC_ERR_INVALID, "nxec_md5_verify_chunks: invalid arguments");
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  // the kernel only reads the digests in verify mode
+  const Md5Region r{d_base, chunk_stride, stripe_stride, len, nstripes, const_cast<unsigned char *>(d_expected),
+                    int64_t(nchunks) * 16, nchunks};
+  return launch_md5(&r, 1, pick_stream(ctx, stream), d_ok, d_nbad);
+}
+
 int nxec_object_layout(int n, int k, int64_t length, int64_t max_chunk_size, int64_t *nstripes,
                        int64_t *full_stripes, int64_t *last_chunk_size) {
   if (!valid_nk(n, k) || length < 0 || max_chunk_size <= 0 || !nstripes || !full_stripes || !last_chunk_size)
@@ -995,6 +1009,171 @@ int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char
   }
   cleanup();
   return NXEC_OK;
+}
+
+namespace {
+
+// Chunk frames <-> device batch: item i of the plan is segment (i % segs) of
+// chunk (i / segs); a piece is up to `per` items staged back to back in one
+// pinned slot.  Chunks longer than a piece are cut into segments.
+constexpr int64_t kFramePiece = int64_t(16) << 20;
+// Pinned frames at least this long are DMA'd one copy per frame; shorter ones
+// are staged too: per-copy overhead holds 1 MiB pinned frames to 34 GiB/s
+// against 50 staged (tools/frames_rate.py).
+constexpr int64_t kFrameDirect = int64_t(8) << 20;
+
+struct FramePlan {
+  int64_t len, seg, segs, per, items, npieces;
+  FramePlan(int64_t nchunks, int64_t l) : len(l) {
+    seg = std::min(len, kFramePiece);
+    segs = (len + seg - 1) / seg;
+    per = std::max<int64_t>(1, kFramePiece / seg);
+    items = nchunks * segs;
+    npieces = (items + per - 1) / per;
+  }
+  int64_t chunk(int64_t i) const { return i / segs; }
+  int64_t off(int64_t i) const { return (i % segs) * seg; }
+  int64_t bytes(int64_t i) const { return std::min(seg, len - off(i)); }
+};
+
+// host memcpy of items [first, first+count) between frames and staging, in
+// jobs of at most 1 MiB spread over the host pool
+void frame_copies(const FramePlan &fp, int64_t first, int64_t count, uint8_t *staging,
+                  const std::function<void(int64_t item, int64_t off, int64_t n, uint8_t *stage)> &copy) {
+  const int64_t job = int64_t(1) << 20;
+  const int64_t jobs_per_item = (fp.seg + job - 1) / job;
+  host_parallel_for(static_cast<int>(count * jobs_per_item), [&](int t) {
+    const int64_t i = t / jobs_per_item, o = (t % jobs_per_item) * job;
+    const int64_t b = fp.bytes(first + i);
+    if (o < b) copy(first + i, o, std::min(job, b - o), staging + i * fp.seg + o);
+  });
+}
+
+// whether every frame is pinned / registered host memory (DMA reads it directly)
+bool frames_pinned(const void *const *frames, int64_t n) {
+  for (int64_t i = 0; i < n; i++) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, frames[i]) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
+int frames_check(nxec_ctx_t *ctx, const void *frames, int64_t nchunks, int64_t len, const void *d, int64_t stride,
+                 const char *what) {
+  if (!ctx || nchunks < 0 || len < 0 || (nchunks > 0 && len > 0 && (!frames || !d || stride < len)))
+    return set_error(NXEC_ERR_INVALID, "%s: invalid arguments", what);
+  return NXEC_OK;
+}
+
+}  // namespace
+
+int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, int64_t nchunks, int64_t len,
+                       unsigned char *d_dst, int64_t dst_stride, void *stream) {
+  int rc = frames_check(ctx, h_chunks, nchunks, len, d_dst, dst_stride, "nxec_gather_chunks");
+  if (rc || nchunks == 0 || len == 0) return rc;
+  if ((rc = ensure_device(ctx->device))) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks)) {
+    for (int64_t i = 0; i < nchunks; i++)
+      NXEC_HIP(hipMemcpyAsync(d_dst + i * dst_stride, h_chunks[i], size_t(len), hipMemcpyHostToDevice, st));
+    NXEC_HIP(hipStreamSynchronize(st));
+    return NXEC_OK;
+  }
+  // pageable frames: the pool packs piece p into one pinned slot while the
+  // copy engine moves piece p-1 out of the other
+  const FramePlan fp(nchunks, len);
+  Slot *slots[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  const size_t cap = size_t(std::min(fp.per, fp.items) * fp.seg);
+  for (int s = 0; s < 2 && rc == NXEC_OK; s++) {
+    if ((rc = acquire_slot(ctx, cap, &slots[s]))) break;
+    rc = hip_check(hipEventCreateWithFlags(&done[s], hipEventDisableTiming), "hipEventCreate");
+  }
+  for (int64_t p = 0; p < fp.npieces && rc == NXEC_OK; p++) {
+    const int s = static_cast<int>(p & 1);
+    const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
+    if (p >= 2 && (rc = hip_check(hipEventSynchronize(done[s]), "gather piece sync"))) break;
+    frame_copies(fp, first, count, slots[s]->h, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
+      std::memcpy(stage, h_chunks[fp.chunk(item)] + fp.off(item) + o, size_t(nb));
+    });
+    hipError_t e = hipSuccess;
+    if (fp.segs == 1) {  // whole chunks: one 2D copy scatters the piece to its strided rows
+      e = hipMemcpy2DAsync(d_dst + fp.chunk(first) * dst_stride, size_t(dst_stride), slots[s]->h, size_t(fp.seg),
+                           size_t(len), size_t(count), hipMemcpyHostToDevice, st);
+    } else {
+      for (int64_t i = first; i < first + count && e == hipSuccess; i++)
+        e = hipMemcpyAsync(d_dst + fp.chunk(i) * dst_stride + fp.off(i), slots[s]->h + (i - first) * fp.seg,
+                           size_t(fp.bytes(i)), hipMemcpyHostToDevice, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(done[s], st);
+    rc = hip_check(e, "gather H2D");
+  }
+  hipError_t e = hipStreamSynchronize(st);  // the slots go back to the pool only once drained
+  if (rc == NXEC_OK) rc = hip_check(e, "gather sync");
+  for (int s = 0; s < 2; s++) {
+    if (done[s]) (void)hipEventDestroy(done[s]);
+    if (slots[s]) release_slot(ctx, slots[s]);
+  }
+  return rc;
+}
+
+int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks, int64_t len,
+                        unsigned char *const *h_chunks, void *stream) {
+  int rc = frames_check(ctx, h_chunks, nchunks, len, d_src, src_stride, "nxec_scatter_chunks");
+  if (rc || nchunks == 0 || len == 0) return rc;
+  if ((rc = ensure_device(ctx->device))) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks)) {
+    for (int64_t i = 0; i < nchunks; i++)
+      NXEC_HIP(hipMemcpyAsync(h_chunks[i], d_src + i * src_stride, size_t(len), hipMemcpyDeviceToHost, st));
+    NXEC_HIP(hipStreamSynchronize(st));
+    return NXEC_OK;
+  }
+  // the copy engine fills piece p+1 into one slot while the pool unpacks piece p
+  const FramePlan fp(nchunks, len);
+  Slot *slots[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  const size_t cap = size_t(std::min(fp.per, fp.items) * fp.seg);
+  for (int s = 0; s < 2 && rc == NXEC_OK; s++) {
+    if ((rc = acquire_slot(ctx, cap, &slots[s]))) break;
+    rc = hip_check(hipEventCreateWithFlags(&done[s], hipEventDisableTiming), "hipEventCreate");
+  }
+  auto issue = [&](int64_t p) {
+    const int s = static_cast<int>(p & 1);
+    const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
+    hipError_t e = hipSuccess;
+    if (fp.segs == 1) {
+      e = hipMemcpy2DAsync(slots[s]->h, size_t(fp.seg), d_src + fp.chunk(first) * src_stride, size_t(src_stride),
+                           size_t(len), size_t(count), hipMemcpyDeviceToHost, st);
+    } else {
+      for (int64_t i = first; i < first + count && e == hipSuccess; i++)
+        e = hipMemcpyAsync(slots[s]->h + (i - first) * fp.seg, d_src + fp.chunk(i) * src_stride + fp.off(i),
+                           size_t(fp.bytes(i)), hipMemcpyDeviceToHost, st);
+    }
+    if (e == hipSuccess) e = hipEventRecord(done[s], st);
+    return hip_check(e, "scatter D2H");
+  };
+  if (rc == NXEC_OK) rc = issue(0);
+  for (int64_t p = 0; p < fp.npieces && rc == NXEC_OK; p++) {
+    const int s = static_cast<int>(p & 1);
+    if (p + 1 < fp.npieces && (rc = issue(p + 1))) break;
+    if ((rc = hip_check(hipEventSynchronize(done[s]), "scatter piece sync"))) break;
+    const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
+    frame_copies(fp, first, count, slots[s]->h, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
+      std::memcpy(h_chunks[fp.chunk(item)] + fp.off(item) + o, stage, size_t(nb));
+    });
+  }
+  hipError_t e = hipStreamSynchronize(st);
+  if (rc == NXEC_OK) rc = hip_check(e, "scatter sync");
+  for (int s = 0; s < 2; s++) {
+    if (done[s]) (void)hipEventDestroy(done[s]);
+    if (slots[s]) release_slot(ctx, slots[s]);
+  }
+  return rc;
 }
 
 int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_object, int64_t length,

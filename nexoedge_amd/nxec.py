@@ -329,6 +329,12 @@ class Context:
         check(lib.nxec_md5_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride, nchunks,
                                   length, nstripes, C.c_void_p(int(digests)), stream), "nxec_md5_chunks")
 
+    def md5_verify_chunks(self, base: int, chunk_stride: int, stripe_stride: int, nchunks: int, length: int,
+                          nstripes: int, expected: int, ok: int, nbad=None, stream=None) -> None:
+        check(lib.nxec_md5_verify_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride,
+                                         nchunks, length, nstripes, C.c_void_p(int(expected)), C.c_void_p(int(ok)),
+                                         C.c_void_p(int(nbad)) if nbad else None, stream), "nxec_md5_verify_chunks")
+
     def encode_object(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int, tail=None,
                       md5=None, stream=None) -> None:
         check(lib.nxec_encode_object(C.c_void_p(self.ptr), n, k, C.c_void_p(int(obj)), length, max_chunk_size,
@@ -376,6 +382,18 @@ class Context:
         check(lib.nxec_rs_encode_host_batch(C.c_void_p(self.ptr), n, k, C.c_void_p(int(h_data)),
                                             C.c_void_p(int(h_parity)), length, nstripes, batch_stripes),
               "nxec_rs_encode_host_batch")
+
+    def gather_chunks(self, frames: Sequence[int], length: int, dst: int, dst_stride: int, stream=None) -> None:
+        """nxec_gather_chunks: host frame addresses -> dst + i*dst_stride (device)."""
+        fp = (C.c_void_p * max(len(frames), 1))(*[int(f) for f in frames])
+        check(lib.nxec_gather_chunks(C.c_void_p(self.ptr), fp, len(frames), length, C.c_void_p(int(dst)), dst_stride,
+                                     stream), "nxec_gather_chunks")
+
+    def scatter_chunks(self, src: int, src_stride: int, frames: Sequence[int], length: int, stream=None) -> None:
+        """nxec_scatter_chunks: src + i*src_stride (device) -> host frame addresses."""
+        fp = (C.c_void_p * max(len(frames), 1))(*[int(f) for f in frames])
+        check(lib.nxec_scatter_chunks(C.c_void_p(self.ptr), C.c_void_p(int(src)), src_stride, len(frames), length, fp,
+                                      stream), "nxec_scatter_chunks")
 
     def describe_launch(self, rows: int, k: int, length: int, nstripes: int) -> str:
         buf = C.create_string_buffer(512)

@@ -388,6 +388,44 @@ def test_md5_chunks_vs_hashlib(gpu_ctx, length):
         db.free()
 
 
+@pytest.mark.parametrize("length,aligned", [(0, True), (65537, False), (1 << 20, True)])
+def test_md5_verify_chunks_flags_corruption(gpu_ctx, length, aligned):
+    """Batch Chunk::verifyMD5 (chunk_manager.cc:1555, container_manager.cc:187):
+    digests from hashlib, a few chunks corrupted on the device (one byte flipped)
+    or given a wrong expected digest -> exactly those flagged, count accumulated."""
+    import hashlib
+    n, ns = 5, 7
+    stride = rup(max(length, 1)) if aligned else max(length, 1) + 3
+    host = fill_bytes(ns * n * stride, 7500 + length).reshape(ns, n, stride)
+    exp = np.zeros((ns, n, 16), dtype=np.uint8)
+    for s in range(ns):
+        for c in range(n):
+            exp[s, c] = np.frombuffer(hashlib.md5(host[s, c, :length].tobytes()).digest(), dtype=np.uint8)
+    bad = {(0, 0), (3, 4), (6, 2)}
+    corrupt = host.copy()
+    for s, c in bad:
+        if length:
+            corrupt[s, c, length // 2] ^= 0x40
+        else:
+            exp[s, c, 5] ^= 1  # empty chunk: wrong expected digest instead
+    sb, eb = up(corrupt), up(exp)
+    ok = nxec.DeviceBuffer(ns * n)
+    nb = nxec.DeviceBuffer(8)
+    nb.memset(0)
+    ok.memset(0x77)
+    for _ in range(2):  # the count accumulates over calls
+        gpu_ctx.md5_verify_chunks(sb.ptr, stride, n * stride, n, length, ns, eb.ptr, ok.ptr, nb.ptr)
+    gpu_ctx.sync()
+    flags = ok.download().reshape(ns, n)
+    want = np.ones((ns, n), dtype=np.uint8)
+    for s, c in bad:
+        want[s, c] = 0
+    assert np.array_equal(flags, want)
+    assert int(nb.download().view(np.uint64)[0]) == 2 * len(bad)
+    for b in (sb, eb, ok, nb):
+        b.free()
+
+
 def test_md5_after_encode_full_batch(gpu_ctx):
     """Write path (chunk_manager.cc:99-175): encode, then MD5 of all n chunks of
     every stripe; sampled digests vs hashlib."""
@@ -817,3 +855,79 @@ def test_rs_encode_host_batch_paths(gpu_ctx, monkeypatch, mode):
     if mode != "pageable":
         hdb.free()
         hpb.free()
+
+
+@pytest.mark.parametrize("nchunks,length,pinned", [
+    (37, 1000, False),             # one piece, odd length
+    (70, (1 << 20) + 3, False),    # several pieces (16 MiB staging)
+    (2, (64 << 20) + 5, False),    # chunks longer than a piece: segments
+    (5, 4097, True),               # short pinned frames: staged
+    (2, (8 << 20) + 3, True),      # long pinned frames: direct DMA
+    (1, 1, False),
+])
+def test_gather_scatter_chunk_frames(gpu_ctx, nchunks, length, pinned):
+    """Chunk frames (misaligned host message buffers) -> strided device batch
+    -> frames again, byte-exact; the device rows' padding is untouched."""
+    pitch = length + 7
+    stride = rup(length) + 32
+    if pinned:
+        hb = nxec.PinnedBuffer(nchunks * pitch + 1)
+        host, base = hb.array, hb.ptr
+    else:
+        host = np.zeros(nchunks * pitch + 1, dtype=np.uint8)
+        base = host.ctypes.data
+    host[:] = fill_bytes(host.size, 7100 + nchunks)
+    frames = [base + 1 + i * pitch for i in range(nchunks)]
+    dev = nxec.DeviceBuffer(nchunks * stride)
+    dev.memset(0xA5)
+    gpu_ctx.sync()
+    gpu_ctx.gather_chunks(frames, length, dev.ptr, stride)
+    got = dev.download().reshape(nchunks, stride)
+    for i in range(nchunks):
+        o = 1 + i * pitch
+        assert np.array_equal(got[i, :length], host[o:o + length]), i
+        assert (got[i, length:] == 0xA5).all(), i
+    out = np.full(nchunks * pitch + 1, 0x3C, dtype=np.uint8)
+    oframes = [out.ctypes.data + 1 + i * pitch for i in range(nchunks)]
+    gpu_ctx.scatter_chunks(dev.ptr, stride, oframes, length)
+    for i in range(nchunks):
+        o = 1 + i * pitch
+        assert np.array_equal(out[o:o + length], host[o:o + length]), i
+        assert (out[o + length:o + pitch] == 0x3C).all(), i
+    dev.free()
+    if pinned:
+        hb.free()
+
+
+def test_decode_from_received_frames(gpu_ctx):
+    """The proxy read path on frames: k surviving chunks arrive as separate
+    message buffers (any order of chunk ids), are gathered into a device stripe
+    batch, decoded, and the data chunks scattered into per-chunk frames equal
+    the original data (oracle-encoded parity)."""
+    n, k, cs, ns = 14, 10, 65536 + 11, 6
+    failed = [1, 4, 11, 13]
+    enc = nxec.gen_rs_matrix(n, k)
+    alive = [c for c in range(n) if c not in failed]
+    data = [fill_bytes(k * cs, 7300 + s).reshape(k, cs) for s in range(ns)]
+    chunks = [np.concatenate([d, np.stack(oracle.matmul(enc[k:], list(d)))]) for d in data]
+    # frames in arrival order: stripe-major, surviving chunk ids shuffled
+    rng = np.random.default_rng(7)
+    order = [(s, c) for s in range(ns) for c in rng.permutation(alive)]
+    msgs = [np.frombuffer(bytes(chunks[s][c]), dtype=np.uint8).copy() for s, c in order]
+    stride = rup(cs)
+    dev = nxec.DeviceBuffer(ns * n * stride)
+    dev.memset(0)
+    # frame i lands at row (stripe, chunk id) of the batch: one gather per chunk id
+    for c in alive:
+        idx = [i for i, (s, cc) in enumerate(order) if cc == c]
+        gpu_ctx.gather_chunks([msgs[i].ctypes.data for i in idx], cs, dev.ptr + c * stride, n * stride)
+    out = nxec.DeviceBuffer(ns * k * stride)
+    gpu_ctx.rs_decode(n, k, failed, dev.ptr, stride, n * stride, out.ptr, stride, k * stride, cs, ns)
+    gpu_ctx.sync()
+    frames = [np.zeros(cs, dtype=np.uint8) for _ in range(ns * k)]
+    gpu_ctx.scatter_chunks(out.ptr, stride, [f.ctypes.data for f in frames], cs)
+    for s in range(ns):
+        for j in range(k):
+            assert np.array_equal(frames[s * k + j], data[s][j]), (s, j)
+    dev.free()
+    out.free()

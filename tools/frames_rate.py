@@ -1,0 +1,87 @@
+"""Chunk-frame gather / scatter rates (nxec_gather_chunks / nxec_scatter_chunks):
+pageable and pinned frames, 1 MiB chunks, alone and with concurrent callers.
+Run on the GPU box: python tools/frames_rate.py"""
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nexoedge_amd import nxec  # noqa: E402
+
+GIB = float(1 << 30)
+cs, nchunks, reps = 1 << 20, 1280, 3
+
+
+def run(ctx, frames, dev, op):
+    for _ in range(reps):
+        if op == "gather":
+            ctx.gather_chunks(frames, cs, dev.ptr, cs)
+        else:
+            ctx.scatter_chunks(dev.ptr, cs, frames, cs)
+
+
+def timed(jobs):
+    ths = [threading.Thread(target=run, args=j) for j in jobs]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return len(jobs) * reps * nchunks * cs / (time.perf_counter() - t0) / GIB
+
+
+def setup(callers, pinned):
+    ctxs, devs, bufs, frames = [], [], [], []
+    for _ in range(callers):
+        ctxs.append(nxec.Context(0))
+        devs.append(nxec.DeviceBuffer(nchunks * cs))
+        if pinned:
+            b = nxec.PinnedBuffer(nchunks * cs)
+            base = b.ptr
+        else:
+            b = np.ones(nchunks * cs, dtype=np.uint8)
+            base = b.ctypes.data
+        bufs.append(b)
+        frames.append([base + i * cs for i in range(nchunks)])
+    return ctxs, devs, bufs, frames
+
+
+def teardown(ctxs, devs, bufs, pinned):
+    for d in devs:
+        d.free()
+    if pinned:
+        for b in bufs:
+            b.free()
+    for c in ctxs:
+        c.close()
+
+
+def rate(callers, op, pinned):
+    ctxs, devs, bufs, frames = setup(callers, pinned)
+    jobs = [(ctxs[i], frames[i], devs[i], op) for i in range(callers)]
+    for j in jobs:
+        run(*j)
+    r = timed(jobs)
+    teardown(ctxs, devs, bufs, pinned)
+    return r
+
+
+def duplex():
+    """one caller gathers while another scatters (both PCIe directions)"""
+    ctxs, devs, bufs, frames = setup(2, False)
+    jobs = [(ctxs[0], frames[0], devs[0], "gather"), (ctxs[1], frames[1], devs[1], "scatter")]
+    for j in jobs:
+        run(*j)
+    r = timed(jobs)
+    teardown(ctxs, devs, bufs, False)
+    return r
+
+
+for pinned in (False, True):
+    for op in ("gather", "scatter"):
+        for callers in (1, 2, 4):
+            print(f"{op:8s} pinned={pinned!s:5s} callers={callers}: {rate(callers, op, pinned):6.2f} GiB/s", flush=True)
+print(f"duplex gather+scatter pageable: {duplex():6.2f} GiB/s", flush=True)
