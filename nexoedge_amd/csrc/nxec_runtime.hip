@@ -170,6 +170,37 @@ static int hip_check(hipError_t e, const char *what) { return e == hipSuccess ? 
 
 using namespace nxec;
 
+namespace {
+// Device staging of the batched host entry points (nxec_encode_object_host,
+// nxec_rs_encode_host_batch), kept across calls (allocating ~4 GiB per call
+// cost ~12 ms of a 150 ms call): kObjSlots batches in flight, one stream and
+// one H2D-done event each.  The context's own stream serves as slot 0: HIP
+// has 4 hardware queues per process (GPU_MAX_HW_QUEUES), and a fifth stream
+// shares one, serialising two slots' copies (object write 44 -> 34 GiB/s).
+constexpr int kObjSlots = 3;
+struct ObjStage {
+  uint8_t *d = nullptr;
+  size_t cap = 0;  // bytes per slot
+  hipStream_t streams[kObjSlots] = {};
+  hipEvent_t h2d_done[kObjSlots] = {};
+  bool borrowed0 = false;  // streams[0] is the context's stream
+  void release() {
+    for (int i = 0; i < kObjSlots; i++) {
+      if (streams[i]) {
+        (void)hipStreamSynchronize(streams[i]);
+        if (i > 0 || !borrowed0) (void)hipStreamDestroy(streams[i]);
+      }
+      if (h2d_done[i]) (void)hipEventDestroy(h2d_done[i]);
+      streams[i] = nullptr;
+      h2d_done[i] = nullptr;
+    }
+    if (d) (void)hipFree(d);
+    d = nullptr;
+    cap = 0;
+  }
+};
+}  // namespace
+
 struct nxec_ctx {
   int device = 0;
   int num_cus = 0;
@@ -177,6 +208,8 @@ struct nxec_ctx {
   std::mutex slot_mu;
   std::vector<Slot *> free_slots;
   std::vector<Slot *> all_slots;
+  std::mutex obj_mu;  // guards obj (one object host call at a time uses it)
+  ObjStage obj;
 };
 
 namespace {
@@ -247,6 +280,35 @@ int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
 void release_slot(nxec_ctx_t *ctx, Slot *s) {
   std::lock_guard<std::mutex> lk(ctx->slot_mu);
   ctx->free_slots.push_back(s);
+}
+
+// The context's persistent batch staging (kObjSlots slots of at least
+// slot_bytes, grown on demand), or a private one in `priv` while another call
+// holds the context's; the caller releases `priv` when it did not get the lock.
+int batch_stage(nxec_ctx_t *ctx, size_t slot_bytes, std::unique_lock<std::mutex> &lk, ObjStage &priv,
+                ObjStage **out) {
+  lk = std::unique_lock<std::mutex>(ctx->obj_mu, std::try_to_lock);
+  ObjStage &stg = lk.owns_lock() ? ctx->obj : priv;
+  slot_bytes = (slot_bytes + 255) / 256 * 256;
+  if (stg.cap < slot_bytes) {
+    stg.release();
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(&stg.d), slot_bytes * kObjSlots);
+    stg.borrowed0 = lk.owns_lock();
+    for (int i = 0; i < kObjSlots && e == hipSuccess; i++) {
+      if (i == 0 && stg.borrowed0)
+        stg.streams[0] = ctx->stream;
+      else
+        e = hipStreamCreateWithFlags(&stg.streams[i], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&stg.h2d_done[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+      stg.release();
+      return hip_err(e, "batch staging allocation");
+    }
+    stg.cap = slot_bytes;
+  }
+  *out = &stg;
+  return NXEC_OK;
 }
 
 std::mutex g_default_mu;
@@ -400,6 +462,7 @@ int nxec_ctx_create(int device, nxec_ctx_t **out) {
 void nxec_ctx_destroy(nxec_ctx_t *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  ctx->obj.release();  // before the context stream it borrows
   if (ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -951,64 +1014,43 @@ int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char
   }
   if (batch_stripes <= 0) batch_stripes = std::max<int64_t>(1, (int64_t(256) << 20) / (len * n));
   batch_stripes = std::min(batch_stripes, nstripes);
+  const int64_t nbatches = (nstripes + batch_stripes - 1) / batch_stripes;
+  batch_stripes = (nstripes + nbatches - 1) / nbatches;  // equal batches
   std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
   nxec_gf_gen_rs_matrix(enc.data(), n, k);
-  constexpr int kSlots = 3;
   const size_t dbytes = static_cast<size_t>(batch_stripes) * k * len, pbytes = static_cast<size_t>(batch_stripes) * p * len;
-  uint8_t *dbuf[kSlots] = {}, *pbuf[kSlots] = {};
-  hipStream_t streams[kSlots] = {};
-  auto cleanup = [&]() {
-    for (int i = 0; i < kSlots; i++) {
-      if (streams[i]) {
-        (void)hipStreamSynchronize(streams[i]);
-        (void)hipStreamDestroy(streams[i]);
-      }
-      if (dbuf[i]) (void)hipFree(dbuf[i]);
-      if (pbuf[i]) (void)hipFree(pbuf[i]);
-    }
-  };
-  for (int i = 0; i < kSlots; i++) {
-    hipError_t e = hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&dbuf[i]), dbytes);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&pbuf[i]), pbytes);
-    if (e != hipSuccess) {
-      cleanup();
-      return hip_err(e, "encode_host_batch setup");
-    }
+  std::unique_lock<std::mutex> lk;
+  ObjStage priv, *pstg = nullptr;
+  if ((rc = batch_stage(ctx, dbytes + pbytes, lk, priv, &pstg))) return rc;
+  ObjStage &stg = *pstg;
+  int prev = -1;
+  for (int64_t b = 0; b < nbatches && rc == NXEC_OK; b++) {
+    const int slot = static_cast<int>(b % kObjSlots);
+    const int64_t s0 = b * batch_stripes, ns = std::min(batch_stripes, nstripes - s0);
+    hipStream_t st = stg.streams[slot];
+    uint8_t *dbuf = stg.d + slot * stg.cap, *pbuf = dbuf + dbytes;
+    // H2D copies one batch after another, so the first batch's kernel starts early
+    if (prev >= 0) rc = hip_check(hipStreamWaitEvent(st, stg.h2d_done[prev], 0), "H2D order");
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(dbuf, h_data + s0 * k * len, static_cast<size_t>(ns) * k * len,
+                                    hipMemcpyHostToDevice, st),
+                     "H2D");
+    if (!rc) rc = hip_check(hipEventRecord(stg.h2d_done[slot], st), "H2D event");
+    prev = slot;
+    if (!rc)
+      rc = nxec_stripes_mul(ctx, p, k, enc.data() + static_cast<size_t>(k) * k, dbuf, nullptr, len, k * len, pbuf,
+                            nullptr, len, p * len, nullptr, len, ns, st);
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(h_parity + s0 * p * len, pbuf, static_cast<size_t>(ns) * p * len,
+                                    hipMemcpyDeviceToHost, st),
+                     "D2H");
   }
-  int64_t b = 0;
-  for (int64_t s0 = 0; s0 < nstripes; s0 += batch_stripes, b++) {
-    const int slot = static_cast<int>(b % kSlots);
-    const int64_t ns = std::min(batch_stripes, nstripes - s0);
-    hipStream_t st = streams[slot];
-    hipError_t e = hipMemcpyAsync(dbuf[slot], h_data + s0 * k * len, static_cast<size_t>(ns) * k * len,
-                                  hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) {
-      cleanup();
-      return hip_err(e, "H2D");
-    }
-    rc = nxec_stripes_mul(ctx, p, k, enc.data() + static_cast<size_t>(k) * k, dbuf[slot], nullptr, len, k * len,
-                          pbuf[slot], nullptr, len, p * len, nullptr, len, ns, st);
-    if (rc) {
-      cleanup();
-      return rc;
-    }
-    e = hipMemcpyAsync(h_parity + s0 * p * len, pbuf[slot], static_cast<size_t>(ns) * p * len, hipMemcpyDeviceToHost,
-                       st);
-    if (e != hipSuccess) {
-      cleanup();
-      return hip_err(e, "D2H");
-    }
+  for (int i = 0; i < kObjSlots; i++) {
+    hipError_t e = hipStreamSynchronize(stg.streams[i]);
+    if (!rc) rc = hip_check(e, "encode_host_batch sync");
   }
-  for (int i = 0; i < kSlots; i++) {
-    hipError_t e = hipStreamSynchronize(streams[i]);
-    if (e != hipSuccess) {
-      cleanup();
-      return hip_err(e, "encode_host_batch sync");
-    }
-  }
-  cleanup();
-  return NXEC_OK;
+  if (!lk.owns_lock()) priv.release();
+  return rc;
 }
 
 namespace {
@@ -1196,78 +1238,70 @@ int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *
   std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
   nxec_gf_gen_rs_matrix(enc.data(), n, k);
   const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
-  constexpr int kSlots = 3;
+  // equal batches: a short last batch would add one whole MD5 chain time
+  // (~10 ms for 1 MiB chunks) after everything else has drained
+  const int64_t nbatches = (nst + batch_stripes - 1) / batch_stripes;
+  batch_stripes = (nst + nbatches - 1) / nbatches;
   const size_t dbytes = size_t(batch_stripes) * k * M, pbytes = size_t(batch_stripes) * std::max(p, 1) * M,
                mbytes = size_t(batch_stripes) * n * 16;
-  uint8_t *dbuf[kSlots] = {}, *pbuf[kSlots] = {}, *mbuf[kSlots] = {};
-  hipStream_t streams[kSlots] = {};
-  auto cleanup = [&]() {
-    for (int i = 0; i < kSlots; i++) {
-      if (streams[i]) {
-        (void)hipStreamSynchronize(streams[i]);
-        (void)hipStreamDestroy(streams[i]);
-      }
-      if (dbuf[i]) (void)hipFree(dbuf[i]);
-      if (pbuf[i]) (void)hipFree(pbuf[i]);
-      if (mbuf[i]) (void)hipFree(mbuf[i]);
-    }
-  };
-  for (int i = 0; i < kSlots; i++) {
-    hipError_t e = hipStreamCreateWithFlags(&streams[i], hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&dbuf[i]), dbytes);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&pbuf[i]), pbytes);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&mbuf[i]), mbytes);
-    if (e != hipSuccess) {
-      cleanup();
-      return hip_err(e, "encode_object_host setup");
-    }
-  }
+  std::unique_lock<std::mutex> lk;
+  ObjStage priv, *pstg = nullptr;
+  if ((rc = batch_stage(ctx, dbytes + pbytes + mbytes, lk, priv, &pstg))) return rc;
+  ObjStage &stg = *pstg;
   const int64_t ds = int64_t(n) * 16;
-  int64_t b = 0;
-  for (int64_t s0 = 0; s0 < nst && rc == NXEC_OK; s0 += batch_stripes, b++) {
-    const int slot = static_cast<int>(b % kSlots);
-    hipStream_t st = streams[slot];
-    const int64_t nb = std::min(batch_stripes, nst - s0);
+  int prev = -1;
+  for (int64_t b = 0; b < nbatches && rc == NXEC_OK; b++) {
+    const int slot = static_cast<int>(b % kObjSlots);
+    hipStream_t st = stg.streams[slot];
+    uint8_t *dbuf = stg.d + slot * stg.cap, *pbuf = dbuf + dbytes, *mbuf = pbuf + pbytes;
+    const int64_t s0 = b * batch_stripes, nb = std::min(batch_stripes, nst - s0);
     const int64_t nfull = std::max<int64_t>(0, std::min(nb, nf - s0));  // full stripes in this batch
     const bool tail = s0 + nb > nf;
+    // H2D copies run one batch after another (concurrent ones share the link
+    // and would delay the first batch's compute)
+    if (prev >= 0) rc = hip_check(hipStreamWaitEvent(st, stg.h2d_done[prev], 0), "H2D order");
     // data: the full stripes are one contiguous run of the object
-    if (nfull > 0)
-      rc = hip_check(hipMemcpyAsync(dbuf[slot], h_object + s0 * k * M, size_t(nfull) * k * M, hipMemcpyHostToDevice, st),
+    if (!rc && nfull > 0)
+      rc = hip_check(hipMemcpyAsync(dbuf, h_object + s0 * k * M, size_t(nfull) * k * M, hipMemcpyHostToDevice, st),
                      "H2D");
-    uint8_t *dtail = dbuf[slot] + nfull * k * M;
+    uint8_t *dtail = dbuf + nfull * k * M;
     const int64_t rem = length - nf * k * M;
     if (!rc && tail) {
       rc = hip_check(hipMemsetAsync(dtail, 0, size_t(k) * cs_last, st), "tail pad");
       if (!rc) rc = hip_check(hipMemcpyAsync(dtail, h_object + nf * k * M, rem, hipMemcpyHostToDevice, st), "tail H2D");
     }
+    if (!rc) rc = hip_check(hipEventRecord(stg.h2d_done[slot], st), "H2D event");
+    prev = slot;
     if (!rc && p > 0 && nfull > 0)
-      rc = nxec_stripes_mul(ctx, p, k, prow, dbuf[slot], nullptr, M, k * M, pbuf[slot], nullptr, M, p * M, nullptr, M,
-                            nfull, st);
+      rc = nxec_stripes_mul(ctx, p, k, prow, dbuf, nullptr, M, k * M, pbuf, nullptr, M, p * M, nullptr, M, nfull, st);
     if (!rc && p > 0 && tail)
-      rc = nxec_stripes_mul(ctx, p, k, prow, dtail, nullptr, cs_last, k * cs_last, pbuf[slot] + nfull * p * M, nullptr,
-                            M, p * M, nullptr, cs_last, 1, st);
+      rc = nxec_stripes_mul(ctx, p, k, prow, dtail, nullptr, cs_last, k * cs_last, pbuf + nfull * p * M, nullptr, M,
+                            p * M, nullptr, cs_last, 1, st);
     if (!rc && h_md5) {
       const Md5Region r[4] = {
-          {dbuf[slot], M, k * M, M, nfull, mbuf[slot], ds, k},
-          {pbuf[slot], M, p * M, M, p > 0 ? nfull : 0, mbuf[slot] + int64_t(k) * 16, ds, p},
-          {dtail, cs_last, k * cs_last, cs_last, tail ? 1 : 0, mbuf[slot] + nfull * ds, ds, k},
-          {pbuf[slot] + nfull * p * M, M, p * M, cs_last, (tail && p > 0) ? 1 : 0,
-           mbuf[slot] + nfull * ds + int64_t(k) * 16, ds, p},
+          {dbuf, M, k * M, M, nfull, mbuf, ds, k},
+          {pbuf, M, p * M, M, p > 0 ? nfull : 0, mbuf + int64_t(k) * 16, ds, p},
+          {dtail, cs_last, k * cs_last, cs_last, tail ? 1 : 0, mbuf + nfull * ds, ds, k},
+          {pbuf + nfull * p * M, M, p * M, cs_last, (tail && p > 0) ? 1 : 0, mbuf + nfull * ds + int64_t(k) * 16, ds,
+           p},
       };
       rc = launch_md5(r, 4, st);
     }
     if (!rc && p > 0 && nfull > 0)
-      rc = hip_check(hipMemcpyAsync(h_parity + s0 * p * M, pbuf[slot], size_t(nfull) * p * M, hipMemcpyDeviceToHost, st),
+      rc = hip_check(hipMemcpyAsync(h_parity + s0 * p * M, pbuf, size_t(nfull) * p * M, hipMemcpyDeviceToHost, st),
                      "D2H");
     if (!rc && p > 0 && tail)  // last stripe: first cs_last bytes of each parity slot
-      rc = hip_check(hipMemcpy2DAsync(h_parity + nf * p * M, M, pbuf[slot] + nfull * p * M, M, cs_last, p,
+      rc = hip_check(hipMemcpy2DAsync(h_parity + nf * p * M, M, pbuf + nfull * p * M, M, cs_last, p,
                                       hipMemcpyDeviceToHost, st),
                      "tail D2H");
     if (!rc && h_md5)
-      rc = hip_check(hipMemcpyAsync(h_md5 + s0 * ds, mbuf[slot], size_t(nb) * ds, hipMemcpyDeviceToHost, st), "md5 D2H");
+      rc = hip_check(hipMemcpyAsync(h_md5 + s0 * ds, mbuf, size_t(nb) * ds, hipMemcpyDeviceToHost, st), "md5 D2H");
   }
-  for (int i = 0; i < kSlots && !rc; i++) rc = hip_check(hipStreamSynchronize(streams[i]), "encode_object_host sync");
-  cleanup();
+  for (int i = 0; i < kObjSlots; i++) {
+    hipError_t e = hipStreamSynchronize(stg.streams[i]);
+    if (!rc) rc = hip_check(e, "encode_object_host sync");
+  }
+  if (!lk.owns_lock()) priv.release();
   return rc;
 }
 

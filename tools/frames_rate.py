@@ -80,6 +80,9 @@ def duplex():
     return r
 
 
+if os.environ.get("FRAMES_QUICK"):  # one pageable gather pass (for a profiler timeline)
+    print(f"gather   pinned=False callers=1: {rate(1, 'gather', False):6.2f} GiB/s", flush=True)
+    sys.exit(0)
 for pinned in (False, True):
     for op in ("gather", "scatter"):
         for callers in (1, 2, 4):
