@@ -507,40 +507,78 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     hp.free()
     hm.free()
     out["read_frames_decode_GiB_s_user_data"] = round(read_from_frames(ctx, n, k, cs, min(ns, 128)), 2)
+    out["recover_frames_zero_copy"] = recover_frames_rate(ctx, n, k, cs, min(ns, 128))
     return out
 
 
-def read_from_frames(ctx, n, k, cs, ns):
+def read_from_frames(ctx, n, k, cs, ns, readers=1):
     """The proxy read path on received chunk frames (pageable message buffers,
     one per chunk): gather the k surviving chunks of every stripe into the
     device batch, full-output decode of 4 erasures, scatter the k data chunks
-    into per-chunk host frames.  User-data GiB/s."""
+    into per-chunk host frames.  `readers` concurrent callers (one context
+    each, like concurrent proxy requests) split the stripes.  User-data GiB/s."""
+    import threading
+
     import numpy as np
 
     failed = list(range(k - (n - k), k))  # worst case: n-k data chunks lost
     alive = [c for c in range(n) if c not in failed]
     rx = np.random.default_rng(2).integers(0, 256, size=ns * k * cs, dtype=np.uint8)
     tx = np.empty(ns * k * cs, dtype=np.uint8)
-    st = nxec.DeviceBuffer(ns * n * cs)
-    dec = nxec.DeviceBuffer(ns * k * cs)
-    rx_frames = {c: [rx.ctypes.data + (s * k + i) * cs for s in range(ns)] for i, c in enumerate(alive)}
-    tx_frames = [tx.ctypes.data + i * cs for i in range(ns * k)]
+    parts = []
+    for r in range(readers):
+        lo, hi = ns * r // readers, ns * (r + 1) // readers
+        c = ctx if r == 0 else nxec.Context(ctx.device)
+        st, dec = nxec.DeviceBuffer((hi - lo) * n * cs), nxec.DeviceBuffer((hi - lo) * k * cs)
+        rxf = {c_: [rx.ctypes.data + (s * k + i) * cs for s in range(lo, hi)] for i, c_ in enumerate(alive)}
+        txf = [tx.ctypes.data + i * cs for i in range(lo * k, hi * k)]
+        parts.append((c, st, dec, rxf, txf, hi - lo))
 
-    def once():
-        for c in alive:
-            ctx.gather_chunks(rx_frames[c], cs, st.ptr + c * cs, n * cs)
-        ctx.rs_decode(n, k, failed, st.ptr, cs, n * cs, dec.ptr, cs, k * cs, cs, ns)
-        ctx.scatter_chunks(dec.ptr, cs, tx_frames, cs)
+    def once(part):
+        c, st, dec, rxf, txf, m = part
+        for cid in alive:
+            c.gather_chunks(rxf[cid], cs, st.ptr + cid * cs, n * cs)
+        c.rs_decode(n, k, failed, st.ptr, cs, n * cs, dec.ptr, cs, k * cs, cs, m)
+        c.scatter_chunks(dec.ptr, cs, txf, cs)
 
-    once()
+    def run_all(reps):
+        th = [threading.Thread(target=lambda p=p: [once(p) for _ in range(reps)]) for p in parts]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
+    run_all(1)
+    reps = 3
+    t0 = time.perf_counter()
+    run_all(reps)
+    dt = (time.perf_counter() - t0) / reps
+    for c, st, dec, _, _, _ in parts:
+        st.free()
+        dec.free()
+        if c is not ctx:
+            c.close()
+    return ns * k * cs / dt / GIB
+
+
+def recover_frames_rate(ctx, n, k, cs, ns):
+    """nxec_rs_recover_frames on pinned frames (a registered receive pool): one
+    kernel reads the k survivors and writes the n-k lost data chunks over PCIe.
+    User data = the k data chunks per stripe now complete in host memory."""
+    e = n - k
+    failed = list(range(k - e, k))
+    buf = nxec.PinnedBuffer(ns * n * cs)
+    buf.array[:] = 7
+    frames = [buf.ptr + i * cs for i in range(ns * n)]
+    ctx.rs_recover_frames(n, k, failed, frames, cs, ns)
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        once()
+        ctx.rs_recover_frames(n, k, failed, frames, cs, ns)
     dt = (time.perf_counter() - t0) / reps
-    st.free()
-    dec.free()
-    return ns * k * cs / dt / GIB
+    buf.free()
+    return {"user_data_GiB_s": round(ns * k * cs / dt / GIB, 2), "pcie_GiB_s_(k+e)cs": round(ns * (k + e) * cs / dt / GIB, 2),
+            "stripes": ns, "failed": failed}
 
 
 def cpu_write_path(args, n, k, cs):

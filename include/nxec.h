@@ -328,6 +328,18 @@ int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, in
 int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks, int64_t len,
                         unsigned char *const *h_chunks, void *stream);
 
+/* RSCode::decode's recover step (rs.cc:111-236 with the rs.cc:238-322 plan) on
+ * chunk frames: frames[s*n + c] is chunk c of stripe s in host memory (len
+ * bytes); the first k alive chunks are read, the `failed` ones written (other
+ * entries may be NULL).  When every frame involved is pinned / registered
+ * host memory (e.g. a receive-buffer pool passed to nxec_host_register) one
+ * kernel reads the survivors and writes the recovered chunks over PCIe through
+ * device pointer tables (zero copy); otherwise the frames are staged through
+ * HBM in batches (nxec_gather_chunks, recover, nxec_scatter_chunks).
+ * Synchronous. */
+int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                           unsigned char *const *frames, int64_t len, int64_t nstripes);
+
 /* ---- Multi-GPU group in one process: one context per device,
  * a batch's stripes split into contiguous ranges (sizes differ by at most one),
  * one host thread per device; no collective, no peer traffic.  Calls are

@@ -1218,6 +1218,84 @@ int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src
   return rc;
 }
 
+int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                           unsigned char *const *frames, int64_t len, int64_t nstripes) {
+  if (!ctx || !valid_nk(n, k) || nfailed < 0 || len < 0 || nstripes < 0 || (nfailed > 0 && !failed) ||
+      (nstripes > 0 && !frames))
+    return set_error(NXEC_ERR_INVALID, "nxec_rs_recover_frames: invalid arguments");
+  if (nfailed == 0 || len == 0 || nstripes == 0) return NXEC_OK;
+  std::vector<int32_t> inputs(n);
+  std::vector<uint8_t> rm(static_cast<size_t>(nfailed) * k);
+  int ni = 0, mi = 0;
+  int rc = nxec_rs_plan(n, k, failed, nfailed, 1, inputs.data(), &ni, &mi, rm.data());  // rs.cc:238-322
+  if (rc) return rc;
+  if ((rc = ensure_device(ctx->device))) return rc;
+  const int e = nfailed, w = k + e;
+  for (int64_t s = 0; s < nstripes; s++) {
+    for (int j = 0; j < k; j++)
+      if (!frames[s * n + inputs[j]]) return set_error(NXEC_ERR_INVALID, "stripe %lld: input frame %d is null", (long long)s, inputs[j]);
+    for (int r = 0; r < e; r++)
+      if (!frames[s * n + failed[r]]) return set_error(NXEC_ERR_INVALID, "stripe %lld: output frame %d is null", (long long)s, failed[r]);
+  }
+  // Zero copy when every frame involved is pinned / registered: one kernel
+  // reads the k survivors and writes the e recovered chunks over PCIe
+  // through device pointer tables ([s][k] inputs, then [s][e] outputs).
+  std::vector<uint64_t> tab(static_cast<size_t>(nstripes) * w);
+  bool direct = true;
+  for (int64_t s = 0; s < nstripes && direct; s++)
+    for (int j = 0; j < w && direct; j++) {
+      const int c = j < k ? inputs[j] : failed[j - k];
+      void *dv = host_device_view(frames[s * n + c]);
+      direct = dv != nullptr;
+      (j < k ? tab[s * k + j] : tab[nstripes * k + s * e + (j - k)]) = reinterpret_cast<uintptr_t>(dv);
+    }
+  if (direct) {
+    Slot *slot = nullptr;
+    if ((rc = acquire_slot(ctx, tab.size() * sizeof(uint64_t), &slot))) return rc;
+    std::memcpy(slot->h, tab.data(), tab.size() * sizeof(uint64_t));
+    rc = hip_check(hipMemcpyAsync(slot->d, slot->h, tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, slot->stream),
+                   "pointer tables H2D");
+    const auto *d_src = reinterpret_cast<const unsigned char *const *>(slot->d);
+    auto *d_dst = reinterpret_cast<unsigned char *const *>(slot->d + size_t(nstripes) * k * sizeof(uint64_t));
+    if (!rc) rc = nxec_stripes_mul_ptrs(ctx, e, k, rm.data(), d_src, d_dst, len, nstripes, slot->stream);
+    hipError_t he = hipStreamSynchronize(slot->stream);
+    if (!rc) rc = hip_check(he, "recover_frames sync");
+    release_slot(ctx, slot);
+    return rc;
+  }
+  // Otherwise staged through HBM in batches: gather the survivors' frames into
+  // [B][k+e][stride], recover rows k.., scatter them to the failed frames.
+  const int64_t stride = (len + 15) / 16 * 16;
+  const int64_t B = std::max<int64_t>(1, std::min<int64_t>(nstripes, (int64_t(256) << 20) / (w * stride)));
+  std::unique_lock<std::mutex> lk;
+  ObjStage priv, *pstg = nullptr;
+  if ((rc = batch_stage(ctx, size_t(B) * w * stride, lk, priv, &pstg))) return rc;
+  uint8_t *d = pstg->d;
+  hipStream_t st = pstg->streams[0];
+  std::vector<int32_t> dst(e);
+  for (int r = 0; r < e; r++) dst[r] = k + r;
+  std::vector<const unsigned char *> in_f(B);
+  std::vector<unsigned char *> out_f(B);
+  for (int64_t s0 = 0; s0 < nstripes && rc == NXEC_OK; s0 += B) {
+    const int64_t nb = std::min(B, nstripes - s0);
+    for (int j = 0; j < k && rc == NXEC_OK; j++) {
+      for (int64_t i = 0; i < nb; i++) in_f[i] = frames[(s0 + i) * n + inputs[j]];
+      rc = nxec_gather_chunks(ctx, in_f.data(), nb, len, d + j * stride, w * stride, st);
+    }
+    if (!rc)
+      rc = nxec_stripes_mul(ctx, e, k, rm.data(), d, nullptr, stride, w * stride, d, dst.data(), stride, w * stride,
+                            nullptr, len, nb, st);
+    for (int r = 0; r < e && rc == NXEC_OK; r++) {
+      for (int64_t i = 0; i < nb; i++) out_f[i] = frames[(s0 + i) * n + failed[r]];
+      rc = nxec_scatter_chunks(ctx, d + (k + r) * stride, w * stride, nb, len, out_f.data(), st);
+    }
+  }
+  hipError_t he = hipStreamSynchronize(st);
+  if (!rc) rc = hip_check(he, "recover_frames sync");
+  if (!lk.owns_lock()) priv.release();
+  return rc;
+}
+
 int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_object, int64_t length,
                             int64_t max_chunk_size, unsigned char *h_parity, unsigned char *h_md5,
                             int64_t batch_stripes) {

@@ -395,6 +395,14 @@ class Context:
         check(lib.nxec_scatter_chunks(C.c_void_p(self.ptr), C.c_void_p(int(src)), src_stride, len(frames), length, fp,
                                       stream), "nxec_scatter_chunks")
 
+    def rs_recover_frames(self, n: int, k: int, failed: Sequence[int], frames: Sequence[int], length: int,
+                          nstripes: int) -> None:
+        """nxec_rs_recover_frames: frames = nstripes*n host addresses ([s][c]; 0 = absent)."""
+        f, fp = _i32(failed)
+        tab = (C.c_void_p * max(len(frames), 1))(*[int(x) if x else None for x in frames])
+        check(lib.nxec_rs_recover_frames(C.c_void_p(self.ptr), n, k, fp, len(failed), tab, length, nstripes),
+              "nxec_rs_recover_frames")
+
     def describe_launch(self, rows: int, k: int, length: int, nstripes: int) -> str:
         buf = C.create_string_buffer(512)
         check(lib.nxec_describe_launch(C.c_void_p(self.ptr), rows, k, length, nstripes, buf, 512), "describe")

@@ -931,3 +931,44 @@ def test_decode_from_received_frames(gpu_ctx):
             assert np.array_equal(frames[s * k + j], data[s][j]), (s, j)
     dev.free()
     out.free()
+
+
+@pytest.mark.parametrize("mode", ["pinned", "registered", "pageable"])
+def test_rs_recover_frames(gpu_ctx, mode):
+    """Recover the failed chunks straight into their host frames: zero copy for
+    pinned / registered frames (interior pointers of one buffer), staged for
+    pageable ones; the recovered frames equal the oracle's chunks, the other
+    frames are untouched."""
+    n, k, cs, ns = 14, 10, 65536 + 5, 7
+    failed = [1, 4, 11, 13]
+    enc = nxec.gen_rs_matrix(n, k)
+    data = [fill_bytes(k * cs, 7600 + s).reshape(k, cs) for s in range(ns)]
+    full = [np.concatenate([d, np.stack(oracle.matmul(enc[k:], list(d)))]) for d in data]
+    pitch = cs + 9
+    size = ns * n * pitch + 3
+    if mode == "pinned":
+        pb = nxec.PinnedBuffer(size)
+        host, base = pb.array, pb.ptr
+    else:
+        host = np.zeros(size, dtype=np.uint8)
+        base = host.ctypes.data
+        if mode == "registered":
+            nxec.check(nxec.lib.nxec_host_register(C.c_void_p(base), size), "register")
+    host[:] = 0x5A
+    frames = []
+    for s in range(ns):
+        for c in range(n):
+            o = 3 + (s * n + c) * pitch
+            if c not in failed:
+                host[o:o + cs] = full[s][c]
+            frames.append(base + o)
+    gpu_ctx.rs_recover_frames(n, k, failed, frames, cs, ns)
+    for s in range(ns):
+        for c in range(n):
+            o = 3 + (s * n + c) * pitch
+            assert np.array_equal(host[o:o + cs], full[s][c]), (s, c)
+            assert (host[o + cs:o + pitch] == 0x5A).all(), (s, c)
+    if mode == "pinned":
+        pb.free()
+    elif mode == "registered":
+        nxec.check(nxec.lib.nxec_host_unregister(C.c_void_p(base)), "unregister")
