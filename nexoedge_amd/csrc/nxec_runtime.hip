@@ -1231,12 +1231,13 @@ int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
   if (rc) return rc;
   if ((rc = ensure_device(ctx->device))) return rc;
   const int e = nfailed, w = k + e;
-  for (int64_t s = 0; s < nstripes; s++) {
-    for (int j = 0; j < k; j++)
-      if (!frames[s * n + inputs[j]]) return set_error(NXEC_ERR_INVALID, "stripe %lld: input frame %d is null", (long long)s, inputs[j]);
-    for (int r = 0; r < e; r++)
-      if (!frames[s * n + failed[r]]) return set_error(NXEC_ERR_INVALID, "stripe %lld: output frame %d is null", (long long)s, failed[r]);
-  }
+  for (int64_t s = 0; s < nstripes; s++)
+    for (int j = 0; j < w; j++) {
+      const int c = j < k ? inputs[j] : failed[j - k];
+      if (!frames[s * n + c])
+        return set_error(NXEC_ERR_INVALID, "nxec_rs_recover_frames: stripe %lld chunk %d frame is null",
+                         static_cast<long long>(s), c);
+    }
   // Zero copy when every frame involved is pinned / registered: one kernel
   // reads the k survivors and writes the e recovered chunks over PCIe
   // through device pointer tables ([s][k] inputs, then [s][e] outputs).
