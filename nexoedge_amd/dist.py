@@ -7,7 +7,9 @@ the max-over-ranks timing reduction.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 from typing import Optional, Tuple
 
 
@@ -18,6 +20,22 @@ def shard_range(nstripes: int, rank: int, world: int) -> Tuple[int, int]:
     base, extra = divmod(nstripes, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Point fd 1 at stderr for the block: gloo's C++ side prints its
+    "[Gloo] Rank r is connected to ..." lines on stdout, where the bench's
+    single JSON result line must be the only output."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 class RankGroup:
@@ -33,7 +51,10 @@ class RankGroup:
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if not dist.is_initialized():
-                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                with _stdout_to_stderr():
+                    dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                    self._dist = dist
+                    self.barrier()  # gloo's mesh is connected (and reported) by now
             self._dist = dist
 
     def barrier(self) -> None:
