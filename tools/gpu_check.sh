@@ -19,12 +19,12 @@ cat $OUT/bench.json
 if [ -n "${PROFILE:-}" ]; then
   cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err || stop rocprof $?
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-inclusive > $OUT/prof_bench.json 2> $OUT/prof.err || stop rocprof $?
   find $OUT/prof -name "*stats*" | head
 fi
 if [ -n "${PMC:-}" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$c -o run -- \
-      python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err || stop pmc_$c $?
+      python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-host-inclusive > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err || stop pmc_$c $?
   done
 fi

@@ -22,7 +22,7 @@ def main():
     print(json.dumps({
         "kernel": f"{sub} (RS(10,4) encode/recover, 4096 stripes x 1 MiB)",
         "source": "rocprofv3 --pmc FETCH_SIZE --kernel-trace and --pmc WRITE_SIZE --kernel-trace, separate passes, "
-                  "python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline (tools/gpu_check.sh PMC=1)",
+                  "python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-host-inclusive (tools/gpu_check.sh PMC=1)",
         "launches": [nf, nw],
         "fetch_size_kb_per_launch": round(f, 2), "write_size_kb_per_launch": round(w, 2),
         "gfx950_correction": "FETCH_SIZE reports half the bytes of a wide coalesced streaming read "
