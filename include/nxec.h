@@ -328,6 +328,25 @@ int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, in
 int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks, int64_t len,
                         unsigned char *const *h_chunks, void *stream);
 
+/* Asynchronous forms: the copy runs on a worker thread and the call returns
+ * at once with a request handle (NULL when the arguments are rejected; the
+ * error is then the return value).  The frame pointer array is copied, the
+ * frames themselves and the device range must stay valid, and the frames
+ * untouched, until nxec_request_wait.  One caller can so overlap receiving
+ * request i+1 (gather, host->device) with sending request i (scatter,
+ * device->host) -- IO::getChunkEventMessage / sendChunkEventMessage
+ * (common/io.cc:104-364) in flight together.  Requests on one stream
+ * serialise on the device: give the two directions different streams
+ * (nxec_stream_create) to use both link directions at once. */
+typedef struct nxec_request nxec_request_t;
+int nxec_gather_chunks_async(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, int64_t nchunks, int64_t len,
+                             unsigned char *d_dst, int64_t dst_stride, void *stream, nxec_request_t **req);
+int nxec_scatter_chunks_async(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks,
+                              int64_t len, unsigned char *const *h_chunks, void *stream, nxec_request_t **req);
+/* Waits for the request, frees it and returns its status (the request's error
+ * message becomes the caller's nxec_last_error).  NULL is a no-op (0). */
+int nxec_request_wait(nxec_request_t *req);
+
 /* RSCode::decode's recover step (rs.cc:111-236 with the rs.cc:238-322 plan) on
  * chunk frames: frames[s*n + c] is chunk c of stripe s in host memory (len
  * bytes); the first k alive chunks are read, the `failed` ones written (other

@@ -74,6 +74,9 @@ _PROTOS = {
     "nxec_gather_chunks": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
     "nxec_scatter_chunks": (C.c_int, [vp, vp, i64, i64, i64, vp, vp]),
     "nxec_rs_recover_frames": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64]),
+    "nxec_gather_chunks_async": (C.c_int, [vp, vp, i64, i64, vp, i64, vp, C.POINTER(vp)]),
+    "nxec_scatter_chunks_async": (C.c_int, [vp, vp, i64, i64, i64, vp, vp, C.POINTER(vp)]),
+    "nxec_request_wait": (C.c_int, [vp]),
     "nxec_rs_plan":(C.c_int, [C.c_int, C.c_int, vp, C.c_int, C.c_int, vp, C.POINTER(C.c_int), C.POINTER(C.c_int), vp]),
     "nxec_rs_decode_matrix": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp]),
     "nxec_device_count": (C.c_int, [C.POINTER(C.c_int)]),

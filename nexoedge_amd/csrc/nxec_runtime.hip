@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -1215,6 +1216,76 @@ int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src
     if (done[s]) (void)hipEventDestroy(done[s]);
     if (slots[s]) release_slot(ctx, slots[s]);
   }
+  return rc;
+}
+
+}  // extern "C"
+
+// One asynchronous frame copy: the synchronous call run on its own thread,
+// its status and error message kept for nxec_request_wait.
+struct nxec_request {
+  std::vector<unsigned char *> frames;  // the caller's frame table, copied
+  std::thread worker;
+  int rc = NXEC_OK;
+  std::string error;
+};
+
+namespace {
+template <class Fn>
+int start_request(const void *frames, int64_t nchunks, Fn &&fn, nxec_request_t **req) {
+  auto *r = new (std::nothrow) nxec_request();
+  if (!r) return set_error(NXEC_ERR_NOMEM, "nxec request: out of memory");
+  const auto *f = static_cast<unsigned char *const *>(frames);
+  r->frames.assign(f, f + nchunks);
+  try {
+    r->worker = std::thread([r, fn]() {
+      r->rc = fn(r->frames.data());
+      if (r->rc != NXEC_OK) r->error = g_last_error;
+    });
+  } catch (const std::system_error &) {
+    delete r;
+    return set_error(NXEC_ERR_HIP, "nxec request: cannot start a worker thread");
+  }
+  *req = r;
+  return NXEC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nxec_gather_chunks_async(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, int64_t nchunks, int64_t len,
+                             unsigned char *d_dst, int64_t dst_stride, void *stream, nxec_request_t **req) {
+  if (!req) return set_error(NXEC_ERR_INVALID, "nxec_gather_chunks_async: null request pointer");
+  *req = nullptr;
+  int rc = frames_check(ctx, h_chunks, nchunks, len, d_dst, dst_stride, "nxec_gather_chunks_async");
+  if (rc) return rc;
+  return start_request(
+      h_chunks, nchunks,
+      [=](unsigned char *const *fr) {
+        return nxec_gather_chunks(ctx, const_cast<const unsigned char *const *>(fr), nchunks, len, d_dst, dst_stride,
+                                  stream);
+      },
+      req);
+}
+
+int nxec_scatter_chunks_async(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src_stride, int64_t nchunks,
+                              int64_t len, unsigned char *const *h_chunks, void *stream, nxec_request_t **req) {
+  if (!req) return set_error(NXEC_ERR_INVALID, "nxec_scatter_chunks_async: null request pointer");
+  *req = nullptr;
+  int rc = frames_check(ctx, h_chunks, nchunks, len, d_src, src_stride, "nxec_scatter_chunks_async");
+  if (rc) return rc;
+  return start_request(
+      h_chunks, nchunks,
+      [=](unsigned char *const *fr) { return nxec_scatter_chunks(ctx, d_src, src_stride, nchunks, len, fr, stream); },
+      req);
+}
+
+int nxec_request_wait(nxec_request_t *req) {
+  if (!req) return NXEC_OK;
+  if (req->worker.joinable()) req->worker.join();
+  const int rc = req->rc;
+  if (rc != NXEC_OK) g_last_error = req->error;
+  delete req;
   return rc;
 }
 

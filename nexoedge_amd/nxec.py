@@ -257,6 +257,22 @@ class Event:
         return float(ms.value)
 
 
+class Request:
+    """Handle of an asynchronous frame copy (nxec_request_t)."""
+
+    def __init__(self, handle: C.c_void_p):
+        self._h = handle
+
+    def wait(self) -> None:
+        h, self._h = self._h, None
+        if h is not None:
+            check(lib.nxec_request_wait(h), "nxec_request_wait")
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            lib.nxec_request_wait(self._h)
+
+
 class Context:
     """An nxec_ctx_t bound to one device: stream + staging pools."""
 
@@ -394,6 +410,24 @@ class Context:
         fp = (C.c_void_p * max(len(frames), 1))(*[int(f) for f in frames])
         check(lib.nxec_scatter_chunks(C.c_void_p(self.ptr), C.c_void_p(int(src)), src_stride, len(frames), length, fp,
                                       stream), "nxec_scatter_chunks")
+
+    def gather_chunks_async(self, frames: Sequence[int], length: int, dst: int, dst_stride: int,
+                            stream=None) -> "Request":
+        """nxec_gather_chunks_async; wait() on the returned request."""
+        fp = (C.c_void_p * max(len(frames), 1))(*[int(f) for f in frames])
+        req = C.c_void_p()
+        check(lib.nxec_gather_chunks_async(C.c_void_p(self.ptr), fp, len(frames), length, C.c_void_p(int(dst)),
+                                           dst_stride, stream, C.byref(req)), "nxec_gather_chunks_async")
+        return Request(req)
+
+    def scatter_chunks_async(self, src: int, src_stride: int, frames: Sequence[int], length: int,
+                             stream=None) -> "Request":
+        """nxec_scatter_chunks_async; wait() on the returned request."""
+        fp = (C.c_void_p * max(len(frames), 1))(*[int(f) for f in frames])
+        req = C.c_void_p()
+        check(lib.nxec_scatter_chunks_async(C.c_void_p(self.ptr), C.c_void_p(int(src)), src_stride, len(frames),
+                                            length, fp, stream, C.byref(req)), "nxec_scatter_chunks_async")
+        return Request(req)
 
     def rs_recover_frames(self, n: int, k: int, failed: Sequence[int], frames: Sequence[int], length: int,
                           nstripes: int) -> None:

@@ -899,6 +899,67 @@ def test_gather_scatter_chunk_frames(gpu_ctx, nchunks, length, pinned):
         hb.free()
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_gather_scatter_async_overlap(gpu_ctx, pinned):
+    """One caller with a gather (request i+1 arriving) and a scatter (request i
+    leaving) in flight together on two streams, then a chain of async
+    requests: every frame byte-exact, the caller's frame table may be
+    released right after the call, errors come back from wait()."""
+    from nexoedge_amd._lib import lib
+
+    nchunks, length = 24, (1 << 20) + 5
+    pitch, stride = length + 3, rup(length)
+    if pinned:
+        hb = nxec.PinnedBuffer(2 * nchunks * pitch)
+        host, base = hb.array, hb.ptr
+    else:
+        host = np.zeros(2 * nchunks * pitch, dtype=np.uint8)
+        base = host.ctypes.data
+    host[:nchunks * pitch] = fill_bytes(nchunks * pitch, 7400 + pinned)
+    src_frames = [base + i * pitch for i in range(nchunks)]
+    out_frames = [base + (nchunks + i) * pitch for i in range(nchunks)]
+    sent = nxec.DeviceBuffer(nchunks * stride)   # request i, already on the device
+    sent.upload(fill_bytes(nchunks * stride, 7450))
+    recv = nxec.DeviceBuffer(nchunks * stride)   # request i+1, arriving
+    s1, s2 = C.c_void_p(), C.c_void_p()
+    assert lib.nxec_stream_create(C.byref(s1)) == 0 and lib.nxec_stream_create(C.byref(s2)) == 0
+    try:
+        gpu_ctx.sync()
+        rg = gpu_ctx.gather_chunks_async(src_frames, length, recv.ptr, stride, stream=s1)
+        rs = gpu_ctx.scatter_chunks_async(sent.ptr, stride, out_frames, length, stream=s2)
+        rs.wait()
+        rg.wait()
+        got = recv.download().reshape(nchunks, stride)
+        want_sent = sent.download().reshape(nchunks, stride)
+        for i in range(nchunks):
+            o = i * pitch
+            assert np.array_equal(got[i, :length], host[o:o + length]), i
+            o2 = (nchunks + i) * pitch
+            assert np.array_equal(host[o2:o2 + length], want_sent[i, :length]), i
+        # a chain: gather -> scatter back to fresh frames, both async on one stream
+        back = np.zeros(nchunks * length, dtype=np.uint8)
+        r1 = gpu_ctx.gather_chunks_async(src_frames, length, recv.ptr, stride, stream=s1)
+        r1.wait()
+        r2 = gpu_ctx.scatter_chunks_async(recv.ptr, stride, [back.ctypes.data + i * length for i in range(nchunks)],
+                                          length, stream=s1)
+        r2.wait()
+        for i in range(nchunks):
+            assert np.array_equal(back[i * length:(i + 1) * length], host[i * pitch:i * pitch + length]), i
+        # argument errors are synchronous: no request is returned
+        req = C.c_void_p(1)
+        rc = lib.nxec_gather_chunks_async(C.c_void_p(gpu_ctx.ptr), None, 3, 16, C.c_void_p(recv.ptr), 16, None,
+                                          C.byref(req))
+        assert rc != 0 and req.value is None and b"invalid" in lib.nxec_last_error()
+        assert lib.nxec_request_wait(None) == 0
+    finally:
+        lib.nxec_stream_destroy(s1)
+        lib.nxec_stream_destroy(s2)
+        sent.free()
+        recv.free()
+        if pinned:
+            hb.free()
+
+
 def test_decode_from_received_frames(gpu_ctx):
     """The proxy read path on frames: k surviving chunks arrive as separate
     message buffers (any order of chunk ids), are gathered into a device stripe

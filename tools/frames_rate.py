@@ -80,6 +80,49 @@ def duplex():
     return r
 
 
+def one_caller_duplex(use_async, pinned=False):
+    """ONE caller moving request i out (scatter) and request i+1 in (gather):
+    sequential synchronous calls vs both async requests in flight on two streams"""
+    from ctypes import byref, c_void_p
+
+    from nexoedge_amd._lib import lib
+    ctxs, devs, bufs, frames = setup(1, pinned)
+    ctx, dev_in, fin = ctxs[0], devs[0], frames[0]
+    dev_out = nxec.DeviceBuffer(nchunks * cs)
+    fout = (np.zeros(nchunks * cs, dtype=np.uint8), )
+    fo = [fout[0].ctypes.data + i * cs for i in range(nchunks)]
+    s1, s2 = c_void_p(), c_void_p()
+    lib.nxec_stream_create(byref(s1))
+    lib.nxec_stream_create(byref(s2))
+
+    def step():
+        if use_async:
+            rg = ctx.gather_chunks_async(fin, cs, dev_in.ptr, cs, stream=s1)
+            rs = ctx.scatter_chunks_async(dev_out.ptr, cs, fo, cs, stream=s2)
+            rg.wait()
+            rs.wait()
+        else:
+            ctx.gather_chunks(fin, cs, dev_in.ptr, cs)
+            ctx.scatter_chunks(dev_out.ptr, cs, fo, cs)
+    step()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    r = 2 * reps * nchunks * cs / (time.perf_counter() - t0) / GIB
+    lib.nxec_stream_destroy(s1)
+    lib.nxec_stream_destroy(s2)
+    dev_out.free()
+    teardown(ctxs, devs, bufs, pinned)
+    return r
+
+
+if os.environ.get("FRAMES_ASYNC"):  # only the one-caller duplex legs
+    for pinned in (False, True):
+        for a in (False, True, False, True):
+            print(f"one caller gather+scatter pinned-in={pinned!s:5s} {'async' if a else 'sync '}: "
+                  f"{one_caller_duplex(a, pinned):6.2f} GiB/s", flush=True)
+    sys.exit(0)
+
 if os.environ.get("FRAMES_QUICK"):  # one pageable gather pass (for a profiler timeline)
     print(f"gather   pinned=False callers=1: {rate(1, 'gather', False):6.2f} GiB/s", flush=True)
     sys.exit(0)
