@@ -101,6 +101,32 @@ static bool run(int n, int k, int cs, bool car) {
   std::printf("DEC %d %d %d %s\n", n, k, cs, out ? sha(out, outSize).c_str() : "-");
   std::free(out);
 
+  // full-output decode for more erasure sets: the last n-k (all parity: every
+  // data chunk comes straight from the inputs) and every single chunk, into a
+  // caller buffer (rs.cc:164-173)
+  {
+    std::vector<std::vector<chunk_id_t>> sets;
+    std::vector<chunk_id_t> last;
+    for (int i = k; i < n; i++) last.push_back(static_cast<chunk_id_t>(i));
+    sets.push_back(last);
+    for (int f = 0; f < n; f++) sets.push_back({static_cast<chunk_id_t>(f)});
+    std::vector<unsigned char> buf(fsize);
+    for (const auto &fs : sets) {
+      plan.release();
+      EXPECT(code->preDecode(fs, plan, nullptr), "preDecode set");
+      std::vector<chunk_id_t> sid = plan.getInputChunkIds();
+      std::vector<Chunk> sin(k);
+      for (int i = 0; i < k; i++) sin[i].copy(stripe[sid[i]]);
+      std::fill(buf.begin(), buf.end(), 0xEE);
+      data_t *bp = buf.data();
+      length_t bsz = 0;
+      EXPECT(code->decode(sin, &bp, bsz, plan, nullptr) && bp == buf.data(), "decode set (%d,%d) first %d", n, k,
+             static_cast<int>(fs[0]));
+      EXPECT(bsz == fsize && std::memcmp(buf.data(), data.data(), fsize) == 0, "decode set content (%d,%d) first %d",
+             n, k, static_cast<int>(fs[0]));
+    }
+  }
+
   // every single-node repair (coding_test.cc:269-427)
   for (int f = 0; f < n; f++) {
     plan.release();
