@@ -882,10 +882,25 @@ struct AgentBatch {
   std::vector<int> reqs;  // request indices staged in this slot (outputs pending)
   size_t out_off = 0, md5_off = 0;
   int64_t stride = 0;
+  size_t d2h_bytes = 0;  // outputs (+ digests) still to be queued device -> host
 };
+
+// Queues a batch's D2H.  Held back until the next batch's H2D is queued: a
+// D2H queued first (it waits for the batch's MD5, ~10 ms) blocked the next
+// batch's H2D on the other stream behind it, so batches ran one after the
+// other (tools/agent_probe.py timeline, profiles/r01_agent_timeline.txt).
+int agent_d2h(AgentBatch &b) {
+  if (!b.d2h_bytes) return NXEC_OK;
+  const size_t nb = b.d2h_bytes;
+  b.d2h_bytes = 0;
+  return hip_check(hipMemcpyAsync(b.slot->h + b.out_off, b.slot->d + b.out_off, nb, hipMemcpyDeviceToHost,
+                                  b.slot->stream),
+                   "agent D2H");
+}
 
 int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
   if (b.reqs.empty()) return NXEC_OK;
+  if (int rc = agent_d2h(b)) return rc;
   NXEC_HIP(hipStreamSynchronize(b.slot->stream));
   const nxec_agent_req &r0 = reqs[b.reqs[0]];
   const int no = r0.noutputs;
@@ -937,7 +952,7 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));
     for (size_t first = 0; first < ids.size() && rc == NXEC_OK; first += B) {
       const int64_t nb = std::min<int64_t>(B, int64_t(ids.size() - first));
-      AgentBatch &b = slots[cur];
+      AgentBatch &b = slots[cur], &other = slots[cur ^ 1];
       cur ^= 1;
       if ((rc = agent_finish(reqs, chunk_size, b))) break;  // this slot's previous batch
       if (!b.slot && (rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
@@ -969,10 +984,8 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
         const Md5Region reg{d_out, stride, no * stride, chunk_size, nb, d_md5, int64_t(no) * 16, no};
         if ((rc = launch_md5(&reg, 1, st))) break;
       }
-      rc = hip_check(hipMemcpyAsync(b.slot->h + b.out_off, d_out, size_t(nb) * (no * stride + (any_md5 ? no * 16 : 0)),
-                                    hipMemcpyDeviceToHost, st),
-                     "agent D2H");
-      if (rc) break;
+      b.d2h_bytes = size_t(nb) * (no * stride + (any_md5 ? no * 16 : 0));
+      if ((rc = agent_d2h(other))) break;  // the previous batch's D2H, behind this batch's H2D
     }
     if (rc) break;
   }
