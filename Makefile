@@ -12,12 +12,12 @@ CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip \
-            $(CSRC)/nxec_group.cpp \
+            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(wildcard $(CSRC)/coding/*.hh)
 
-all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test
+all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test
 
 # rs.cc's ISA-L call sequence compiled against include/nxec_isal_compat.h (plain C)
 build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h $(LIBDIR)/libnxec.so
@@ -28,6 +28,16 @@ build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h 
 build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
+
+# unmodified-ChunkManager repair flow: CodingOptions() fed by the Config bridge
+# (nexoedge_amd/integration/nxec_config_bridge.cc) over a test double of Config
+STUB := tests/cpp/nexoedge_stub/common
+build/chunk_manager_flow_test: tests/cpp/chunk_manager_flow_test.cc nexoedge_amd/integration/nxec_config_bridge.cc \
+                               $(STUB)/config.hh $(LIBDIR)/libnxec.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) -I$(CSRC)/coding -I$(STUB) -I$(STUB)/coding \
+	    tests/cpp/chunk_manager_flow_test.cc nexoedge_amd/integration/nxec_config_bridge.cc \
+	    -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
 
 $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p $(dir $@)

@@ -25,18 +25,20 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import nexoedge_amd  # noqa: E402  (load libnxec before torch: one HIP runtime)
-from nexoedge_amd import nxec  # noqa: E402
-from nexoedge_amd.dist import RankGroup  # noqa: E402
+nxec = None  # nexoedge_amd.nxec, imported in main() (after the rank launcher)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PATTERNS = ([0, 1, 2, 3], [10, 11, 12, 13], [1, 4, 11, 13])
 GIB = float(1 << 30)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (= ranks).  Without WORLD_SIZE in the environment (not under torch.distributed.run) "
+                         "bench.py starts the N rank processes itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks only rendezvous (gloo), reduce and report")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=14)
@@ -44,120 +46,155 @@ def parse():
     ap.add_argument("--chunk", type=int, default=1 << 20)
     ap.add_argument("--stripes", type=int, default=4096, help="stripes per GPU (batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-stripes", type=int, default=192)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: every CPU of this process's affinity mask)")
+    ap.add_argument("--cpu-stripes", type=int, default=192, help="CPU baseline sample (raised to >= one per thread)")
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="min wall time of the SIMD CPU baseline leg")
     ap.add_argument("--cpu-ref-stripes", type=int, default=96, help="stripes for the (slow) reference base-C leg")
     ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true", default=True,
                     help="also time the pinned H2D->encode->D2H pipeline (default on; N=1 headline workload only)")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
-    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files"]), default="rs10_4",
+    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files", "config1"]), default="rs10_4",
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def _cpu_run(threads, ns, fn_enc, fn_rec, min_s):
-    """Time encode-then-recover legs over `ns` stripes on `threads` threads,
-    repeating the pair until at least `min_s` seconds have elapsed."""
+def _cpu_legs(threads, ns, legs, min_s):
+    """Run each leg fn(lo, hi) over `ns` stripes split into `threads` contiguous
+    ranges (one C call per thread and leg: ctypes releases the GIL), legs back
+    to back, repeating the round until at least `min_s` seconds have elapsed.
+    Returns (rounds, [seconds per leg])."""
     import concurrent.futures as cf
 
     bounds = [(ns * t // threads, ns * (t + 1) // threads) for t in range(threads)]
-    reps, enc_s, rec_s = 0, 0.0, 0.0
-    with cf.ThreadPoolExecutor(threads) as ex:
-        while reps == 0 or enc_s + rec_s < min_s:
-            t0 = time.perf_counter()
-            list(ex.map(lambda b: fn_enc(*b), bounds))
-            t1 = time.perf_counter()
-            list(ex.map(lambda b: fn_rec(*b), bounds))
-            t2 = time.perf_counter()
-            enc_s, rec_s, reps = enc_s + t1 - t0, rec_s + t2 - t1, reps + 1
-    return reps, enc_s, rec_s
+    bounds = [b for b in bounds if b[1] > b[0]]
+    reps, secs = 0, [0.0] * len(legs)
+    with cf.ThreadPoolExecutor(len(bounds)) as ex:
+        while reps == 0 or sum(secs) < min_s:
+            for i, fn in enumerate(legs):
+                t0 = time.perf_counter()
+                list(ex.map(lambda b: fn(*b), bounds))
+                secs[i] += time.perf_counter() - t0
+            reps += 1
+    return reps, secs
 
 
 def _host_info():
+    """CPU model, nproc, this process's affinity mask and the cgroup CPU quota
+    (the GPU box runs the bench in a cgroup: `cpu.max` caps the CPU time all
+    threads together get, whatever the affinity mask lists)."""
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
     except OSError:
         pass
-    return {"cpu": model, "nproc": os.cpu_count()}
+    info = {"cpu": model, "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
 
 
 def cpu_baseline(args, n, k, cs):
     """The same encode + (k,e)-recover work on a bounded sample of stripes on the
-    host cores (ctypes calls release the GIL; one stripe per call):
+    host cores, one contiguous stripe range per thread:
 
-    * value: the production-class stand-in for ISA-L's SIMD kernels the
-      reference links (oracle/nxec_cpu_simd.c, split-nibble vpshufb; the faster
-      of its AVX-512BW and AVX2 forms on this host) -- `kind: "port"`;
+    * value: RSCode::encode as the reference runs it per stripe -- the rs.cc:80
+      copy of the k data chunks into the stripe's chunk buffers, then
+      ec_encode_data -- followed by the 4-erasure recover (rs.cc repair rows),
+      with the production-class stand-in for ISA-L's SIMD kernels
+      (oracle/nxec_cpu_simd.c, split-nibble vpshufb, the faster of AVX-512BW /
+      AVX2 here) -- `kind: "port"`.  Threads = this process's CPU affinity
+      mask (`cores`); the cgroup quota that shares them is stated in `host`.
     * reference_base_c: the reference's own ISA-L 2.22 base C built from its
-      tarball (oracle/_ref), the only ISA-L path buildable here (no nasm)."""
+      tarball (oracle/_ref), the only ISA-L path buildable here (no nasm).
+    * reference_read_decode: the reference's read-path decode, all k rows of
+      the k x k inverse (rs.cc:196,228-230), which the recover leg replaces."""
     import numpy as np
 
     import oracle
 
     p, e = n - k, len(PATTERNS[0])
-    ns, threads = args.cpu_stripes, args.cpu_threads
+    info = _host_info()
+    threads = args.cpu_threads or info["affinity"]
+    ns = max(args.cpu_stripes, threads)
     enc = nxec.gen_rs_matrix(n, k)[k:]
     ids, _, rm = nxec.rs_plan(n, k, PATTERNS[0], True)
-    data = oracle.fill_bytes(ns * k * cs, 99).reshape(ns, k, cs)
-    parity = np.zeros((ns, p, cs), dtype=np.uint8)
-    rec = np.zeros((ns, e, cs), dtype=np.uint8)
+    ids = ids[:k]
+    # uniform random bytes (the SIMD path has no data-dependent timing): one
+    # random stripe, replicated
+    one = oracle.fill_bytes(k * cs, 99).reshape(1, k, cs)
+    data = np.empty((ns, k, cs), dtype=np.uint8)
+    data[:] = one
+    chunks = np.zeros((ns, n, cs), dtype=np.uint8)
+    rec = np.zeros((ns, max(e, k), cs), dtype=np.uint8)
     stripe_bytes = (k + p) * cs + (k + e) * cs
 
-    def survivors(s):
-        st = (list(data[s]) + list(parity[s]))
-        return [st[i] for i in ids[:k]]
-
-    def leg(encode_fn):
-        def fe(lo, hi):
-            for s in range(lo, hi):
-                encode_fn(enc, list(data[s]), list(parity[s]))
-
-        def fr(lo, hi):
-            for s in range(lo, hi):
-                encode_fn(rm, survivors(s), list(rec[s]))
-        return fe, fr
+    def legs(level):
+        fe = lambda lo, hi: oracle.simd_rscode_encode_range(level, n, k, cs, lo, hi, data, chunks, enc)  # noqa: E731
+        fr = lambda lo, hi: oracle.simd_rscode_decode_range(level, n, k, cs, lo, hi, chunks, ids, rm, rec)  # noqa: E731
+        return [fe, fr]
 
     best = None
     top = oracle.simd_level()
     for level in sorted({lv for lv in (top, 256) if 0 < lv <= top}, reverse=True):
-        fe, fr = leg(lambda c, src, dst, lv=level: oracle.simd_encode(c, src, dst, lv))
-        reps, es, rs_ = _cpu_run(threads, ns, fe, fr, args.cpu_seconds)
+        reps, (es, rs_) = _cpu_legs(threads, ns, legs(level), args.cpu_seconds)
         gibs = reps * ns * stripe_bytes / (es + rs_) / GIB
         if best is None or gibs > best[0]:
             best = (gibs, level, reps, es, rs_)
-    sample = (f"RS(10,4) (n,k)=({n},{k}) {cs >> 10} KiB chunks, {ns} stripes x {best[2]} passes: encode then "
-              f"recover {PATTERNS[0]} (rs.cc repair rows), {threads} threads over stripes")
+    gibs, level, reps, es, rs_ = best
+    sample = (f"RS(10,4) (n,k)=({n},{k}) {cs >> 10} KiB chunks, {ns} stripes x {reps} passes: RSCode::encode (rs.cc:80 "
+              f"copy of the data chunks + parity) then recover {PATTERNS[0]} (rs.cc repair rows), {threads} threads, "
+              f"one contiguous stripe range each")
     out = {
-        "value": round(best[0], 3),
+        "value": round(gibs, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": sample + f"; split-nibble vpshufb {'AVX-512BW' if best[1] == 512 else 'AVX2'} stand-in for "
+        "sample": sample + f"; split-nibble vpshufb {'AVX-512BW' if level == 512 else 'AVX2'} stand-in for "
                            "ISA-L's SIMD ec_encode_data (oracle/nxec_cpu_simd.c)",
-        "encode_s": round(best[3], 3),
-        "decode_s": round(best[4], 3),
+        "encode_s": round(es, 3),
+        "decode_s": round(rs_, 3),
+        "host": info,
     }
-    # one thread of the same port, and the host it ran on (SURVEY 8d)
+    # the same legs at the cgroup's CPU count and on one thread (SURVEY 8d)
+    quota = info.get("cgroup_cpu_quota")
+    if quota and int(quota) != threads:
+        tq = max(1, int(quota))
+        r2, (e2, d2) = _cpu_legs(tq, ns, legs(level), 1.0)
+        out["at_cgroup_quota"] = {"threads": tq, "value": round(r2 * ns * stripe_bytes / (e2 + d2) / GIB, 3)}
     nss = min(ns, 16)
-    fe, fr = leg(lambda c, src, dst, lv=best[1]: oracle.simd_encode(c, src, dst, lv))
-    reps, es, rs_ = _cpu_run(1, nss, fe, fr, 1.0)
-    out["single_thread"] = round(reps * nss * stripe_bytes / (es + rs_) / GIB, 3)
-    out["host"] = _host_info()
+    r1, (e1, d1) = _cpu_legs(1, nss, legs(level), 1.0)
+    out["single_thread"] = round(r1 * nss * stripe_bytes / (e1 + d1) / GIB, 3)
+    # the reference's read decode: all k rows of the inverse (rs.cc:228-230)
+    inv = nxec.decode_matrix(n, k, ids, list(range(k)))
+    fd = lambda lo, hi: oracle.simd_rscode_decode_range(level, n, k, cs, lo, hi, chunks, ids, inv, rec)  # noqa: E731
+    r3, (d3,) = _cpu_legs(threads, ns, [fd], 1.0)
+    out["reference_read_decode"] = {"value": round(r3 * ns * (k + e) * cs / d3 / GIB, 3), "unit": "GiB/s (k+e)*cs",
+                                    "note": "rs.cc decode: k x k inverse applied to all k rows, SIMD port"}
     if oracle.ref_available():
         ref = oracle.RefISAL()
-        nsr = min(ns, args.cpu_ref_stripes)
-        fe, fr = leg(ref.encode)
-        reps, es, rs_ = _cpu_run(threads, nsr, fe, fr, 0.0)
+        nsr = max(min(ns, args.cpu_ref_stripes), min(threads, ns))
+
+        def rfe(lo, hi):
+            for s in range(lo, hi):
+                ref.encode(enc, list(data[s]), list(chunks[s, k:]))
+
+        def rfr(lo, hi):
+            for s in range(lo, hi):
+                ref.encode(rm, [chunks[s, i] for i in ids], list(rec[s, :e]))
+        r4, (e4, d4) = _cpu_legs(threads, nsr, [rfe, rfr], 0.0)
         out["reference_base_c"] = {
-            "value": round(reps * nsr * stripe_bytes / (es + rs_) / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "reference", "sample": f"{nsr} stripes, same work; ISA-L 2.22 ec_base.c built from the "
-                                           "reference tarball (pure C)"}
+            "value": round(r4 * nsr * stripe_bytes / (e4 + d4) / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "reference", "sample": f"{nsr} stripes, same work (without the rs.cc:80 copy); ISA-L 2.22 "
+                                           "ec_base.c built from the reference tarball (pure C)"}
     return out
 
 
@@ -202,8 +239,9 @@ def wl_rs10_4(args, ctx, stream, rank):
         "byte_accounting": "encode (k+p)*cs + decode (k+e)*cs per stripe (ISA-L erasure_code_perf.c)",
         "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
     }
+    kern = config["launch"]["kernel"]
     return Workload("rs10_4", "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident", config, ops, [buf],
-                    f"k_mul_vec<K={k},R=8> work-queue (encode launch)", ns)
+                    f"{kern} K={k} rows={p} work-queue (encode launch)", ns)
 
 
 def wl_repair12(args, ctx, stream, rank):
@@ -233,8 +271,9 @@ def wl_repair12(args, ctx, stream, rank):
               "stripes_per_gpu": ns, "chunk_bytes": cs,
               "byte_accounting": "fused (k+1)*cs; CAR unfused (k+1+2G)*cs per stripe (SURVEY 8d)",
               "launch": json.loads(ctx.describe_launch(1, k, cs, ns))}
+    kern = config["launch"]["kernel"]
     return Workload("repair12", "GiB/s RS(12,4) single-failure repair, 1 MiB chunks, device-resident", config, ops,
-                    [buf, part], "k_mul_vec<K=12,R=8> (fused recover, rows=1)", ns)
+                    [buf, part], f"{kern} K={k} rows=1 (fused recover)", ns)
 
 
 def wl_mixed16(args, ctx, stream, rank):
@@ -343,14 +382,179 @@ def wl_files(args, ctx, stream, rank):
                     config, ops, [arena, par, tail, md5], "encode_objects (gather + list + MD5 launches)", total)
 
 
+CONFIG1 = ((6, 4, 1 << 20, "RS(4,2) read as (n,k)=(6,4), 4 MiB file, 1 MiB chunks"),
+           (4, 2, 2 << 20, "literal sample storage_class.ini (n,k)=(4,2), 4 MiB file, 2 MiB chunks"))
+
+
+def wl_config1(args, ctx, stream, rank):
+    """Config 1: a 4 MiB file, one stripe, in both readings of RS(4,2) (SURVEY
+    §0): (n,k)=(6,4) with 1 MiB chunks and the sample's literal (4,2) with
+    2 MiB chunks.  One step = per geometry one encode launch and one
+    (n-k)-erasure recover launch over the single stripe (device-resident; a
+    single stripe is launch-latency bound, not HBM bound).  The CPU legs of
+    the same file (reference base C, SIMD port, per-stripe GPU host path) are
+    in cpu_baseline.by_config."""
+    ops, bufs = [], []
+    for n, k, cs, _ in CONFIG1:
+        buf = nxec.DeviceBuffer(n * cs)
+        buf.fill_random(0x5EED + n + rank)
+        lost = list(range(n - k))
+        ops.append((f"encode_{n}_{k}", lambda i, b=buf, n=n, k=k, cs=cs: ctx.rs_encode(n, k, b.ptr, cs, n * cs, cs, 1,
+                                                                                           stream), (n) * cs))
+        ops.append((f"recover_{n}_{k}", lambda i, b=buf, n=n, k=k, cs=cs, f=lost: ctx.rs_recover(
+            n, k, f, b.ptr, cs, n * cs, cs, 1, stream), (k + len(lost)) * cs))
+        bufs.append(buf)
+    config = {"workload": "config 1: 4 MiB file = one stripe, (n,k)=(6,4) 1 MiB chunks and literal (4,2) 2 MiB "
+                          "chunks; encode + (n-k)-erasure recover per geometry",
+              "geometries": [g[3] for g in CONFIG1],
+              "byte_accounting": "encode n*cs + recover (k+e)*cs per stripe"}
+    return Workload("config1", "GiB/s RS(4,2) 4 MiB-file encode+decode (config 1), device-resident", config, ops,
+                    bufs, "k_mul_vec (single-stripe encode launch, latency bound)", 1)
+
+
+def cpu_baseline_config1(args):
+    """Config 1 on the host: each geometry's 4 MiB file written (RSCode::encode
+    with the rs.cc:80 copy) and read back with the first n-k chunks lost
+    (RSCode::decode: all k rows of the k x k inverse, rs.cc:196,228-230), one
+    file per call on one thread (the proxy codes a file's stripes in
+    sequence), by the reference's ISA-L base C and the SIMD port; plus the
+    same per-file calls through libnxec's host-buffer entry point
+    (nxec_encode_host, the path RSCode::encode/decode take) for comparison."""
+    import numpy as np
+
+    import oracle
+
+    level = oracle.simd_level()
+    ref = oracle.RefISAL() if oracle.ref_available() else None
+    out = {}
+    for n, k, cs, label in CONFIG1:
+        e = n - k
+        enc = nxec.gen_rs_matrix(n, k)[k:]
+        ids, _, _ = nxec.rs_plan(n, k, list(range(e)), False)
+        ids = ids[:k]
+        inv = nxec.decode_matrix(n, k, ids, list(range(k)))
+        data = oracle.fill_bytes(k * cs, 4242 + n).reshape(1, k, cs)
+        chunks = np.zeros((1, n, cs), dtype=np.uint8)
+        dec = np.zeros((1, k, cs), dtype=np.uint8)
+        file_bytes = (n + 2 * k) * cs  # write n*cs + read (k survivors in, k out)
+
+        def timed(fn, min_s=0.5):
+            fn()
+            reps, t0 = 0, time.perf_counter()
+            while reps == 0 or time.perf_counter() - t0 < min_s:
+                fn()
+                reps += 1
+            return (time.perf_counter() - t0) / reps
+
+        def port():
+            oracle.simd_rscode_encode_range(level, n, k, cs, 0, 1, data, chunks, enc)
+            oracle.simd_rscode_decode_range(level, n, k, cs, 0, 1, chunks, ids, inv, dec)
+
+        res = {"file_ms_port_1t": round(timed(port) * 1e3, 3)}
+        if ref is not None:
+            def base_c():
+                ref.encode(enc, list(data[0]), list(chunks[0, k:]))
+                ref.encode(inv, [chunks[0, i] for i in ids], list(dec[0]))
+            res["file_ms_reference_base_c_1t"] = round(timed(base_c) * 1e3, 3)
+
+        def gpu_host():
+            nxec.encode_host(enc, list(data[0]))
+            nxec.encode_host(inv, [chunks[0, i] for i in ids])
+        res["file_ms_gpu_host_path"] = round(timed(gpu_host) * 1e3, 3)
+        for key in list(res):
+            res[key.replace("file_ms", "GiB_s")] = round(file_bytes / (res[key] * 1e-3) / GIB, 3)
+        res["bytes_per_file"] = file_bytes
+        out[label] = res
+    return out
+
+
 WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14,
-             "object": wl_object, "files": wl_files}
+             "object": wl_object, "files": wl_files, "config1": wl_config1}
+
+
+def launch_local_ranks(argv, world):
+    """`bench.py --gpus N` outside torch.distributed.run: start N fresh rank
+    processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, the same argv),
+    one per GPU, before this process has imported the package or touched a
+    GPU.  Rank 0's JSON line is forwarded; the exit status is non-zero if any
+    rank fails (the others are then stopped: a rank blocked in a barrier would
+    never finish)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        # rank 0's stdout is the result; the others' go to stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    failed = None
+    live = set(range(world))
+    out0 = b""
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0 and failed is None:
+                failed = (r, rc)
+                for q in live:  # exact PIDs this launcher started
+                    try:
+                        procs[q].send_signal(signal.SIGTERM)
+                    except OSError:
+                        pass
+        if live:
+            time.sleep(0.05)
+    out0 = procs[0].stdout.read()
+    sys.stdout.write(out0.decode(errors="replace"))
+    sys.stdout.flush()
+    if failed is not None:
+        print(f"bench launcher: rank {failed[0]} exited with status {failed[1]}", file=sys.stderr)
+        return failed[1] if failed[1] > 0 else 1
+    return 0
+
+
+def dry_run(args):
+    """Launcher/rendezvous check without a GPU: the ranks meet over gloo, take
+    the same barrier + max-over-ranks + sum reductions as a real run, and rank
+    0 prints the line shape a real run would (no compute, value null)."""
+    from nexoedge_amd.dist import RankGroup
+
+    if os.environ.get("RANK") == os.environ.get("NXEC_DRY_RUN_FAIL_RANK", "-"):
+        sys.exit(3)  # launcher test: this rank dies before the rendezvous
+    grp = RankGroup()
+    grp.barrier()
+    t = 0.001 * (grp.rank + 1)
+    elapsed = grp.max(t)
+    ranks = grp.sum(1.0)
+    if grp.rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": grp.world, "ranks_seen": int(ranks),
+                          "max_elapsed_s": elapsed, "steps": args.steps, "warmup": args.warmup}), flush=True)
+    grp.close()
 
 
 def main():
+    global nxec
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_local_ranks(sys.argv[1:], args.gpus))
+    if args.dry_run:
+        return dry_run(args)
+    import nexoedge_amd  # noqa: F401  (load libnxec before torch: one HIP runtime)
+    from nexoedge_amd import nxec as _nxec
+    from nexoedge_amd.dist import RankGroup
+
+    nxec = _nxec
     grp = RankGroup()
     world, rank, local = grp.world, grp.rank, grp.local_rank
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one rank per GPU; more ranks than visible GPUs share them round-robin
     # (only for rehearsing the multi-rank path on a small box)
     ctx = nxec.Context(local % max(1, nxec.device_count()))
@@ -456,6 +660,15 @@ def main():
         result["cpu_baseline"] = cpu_baseline(args, args.n, args.k, args.chunk)
         if args.host_inclusive:
             result["cpu_baseline"]["write_path_with_md5"] = cpu_write_path(args, args.n, args.k, args.chunk)
+    if rank == 0 and world == 1 and wl.name == "config1" and not args.no_cpu_baseline:
+        by = cpu_baseline_config1(args)
+        first = by[CONFIG1[0][3]]
+        ref_v = first.get("GiB_s_reference_base_c_1t")
+        result["cpu_baseline"] = {
+            "value": ref_v if ref_v is not None else first["GiB_s_port_1t"], "unit": "GiB/s", "cores": 1,
+            "kind": "reference" if ref_v is not None else "port",
+            "sample": f"one 4 MiB file written and read back, {CONFIG1[0][3]}; both readings in by_config",
+            "by_config": by, "host": _host_info()}
     if rank == 0:
         print(json.dumps(result), flush=True)
     for b in wl.buffers:
@@ -592,7 +805,8 @@ def cpu_write_path(args, n, k, cs):
 
     import oracle
 
-    p, ns, threads = n - k, min(args.cpu_stripes, 64), args.cpu_threads
+    threads = args.cpu_threads or len(os.sched_getaffinity(0))
+    p, ns = n - k, max(min(args.cpu_stripes, 64), threads)
     enc = nxec.gen_rs_matrix(n, k)[k:]
     data = oracle.fill_bytes(ns * k * cs, 7).reshape(ns, k, cs)
     parity = np.zeros((ns, p, cs), dtype=np.uint8)

@@ -415,6 +415,38 @@ int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream);
  * replication, block/grid) -- for benchmarks and logs. */
 int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len);
 
+/* ---------------------------------------------------------------------------
+ * 6. Pinned host arena for chunk buffers (Chunk::allocateData, reference
+ *    chunk.hh:55-66).  Blocks are pinned and device-mapped, recycled by size
+ *    class, never returned to the OS; the arena is bounded by
+ *    NXEC_HOST_ARENA_MAX bytes (default 16 GiB, 0 disables).  nxec_encode_host
+ *    (RSCode::encode, CodingUtils::encode) hands arena buffers to the GPU
+ *    without a staging copy.  nxec_host_alloc fails (NXEC_ERR_NOMEM /
+ *    NXEC_ERR_NODEV) when the arena is full or no device is usable: the
+ *    caller then uses ordinary memory.  Page-aligned.  Thread-safe.
+ * ------------------------------------------------------------------------- */
+int nxec_host_alloc(size_t bytes, void **p);
+/* returns the block to its free list; NXEC_ERR_INVALID if p is not an arena block */
+int nxec_host_free(void *p);
+/* 1 if p is the start of an arena block, else 0 */
+int nxec_host_arena_owns(const void *p);
+int nxec_host_arena_stats(size_t *pinned_bytes, size_t *in_use_bytes);
+/* 1 if the whole host range [p, p + bytes) is pinned / registered memory of
+ * one device mapping -- the test the host entry points apply before letting a
+ * kernel read or write a buffer over PCIe (zero copy) -- else 0 */
+int nxec_host_range_mapped(const void *p, size_t bytes);
+
+/* ---------------------------------------------------------------------------
+ * 7. Recovery and testing hooks.
+ * ------------------------------------------------------------------------- */
+/* Zero every work-queue slot of the calling thread's current device
+ * (synchronous).  Failed launches reset their own slot; this is for recovery
+ * after a device error left launches unfinished. */
+int nxec_reset_work_queues(void);
+/* Testing only: store `next_tile` in the tile counter of the slot the next
+ * coding launch will draw (simulates a launch that died mid-flight). */
+int nxec_debug_poison_next_queue_slot(uint32_t next_tile);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,6 +103,13 @@ _PROTOS = {
     "nxec_fill_random": (C.c_int, [vp, C.c_size_t, C.c_uint64, vp]),
     "nxec_checksum": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), vp]),
     "nxec_describe_launch": (C.c_int, [vp, C.c_int, C.c_int, i64, i64, C.c_char_p, C.c_int]),
+    "nxec_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(vp)]),
+    "nxec_host_free": (C.c_int, [vp]),
+    "nxec_host_arena_owns": (C.c_int, [vp]),
+    "nxec_host_arena_stats": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "nxec_host_range_mapped": (C.c_int, [vp, C.c_size_t]),
+    "nxec_reset_work_queues": (C.c_int, []),
+    "nxec_debug_poison_next_queue_slot": (C.c_int, [C.c_uint32]),
     "nxec_group_create": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
     "nxec_group_destroy": (None, [vp]),
     "nxec_group_size": (C.c_int, [vp]),

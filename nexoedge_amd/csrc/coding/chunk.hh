@@ -1,56 +1,146 @@
-// Chunk buffer as the coding layer sees it (reference: src/ds/chunk.hh:15-130,
-// reduced to the fields RSCode touches: id, data, size, ownership).  File
-// identity, versions and MD5 belong to the proxy/agent and stay there.
+// Chunk: a chunk buffer plus its identity and checksum (reference:
+// src/ds/chunk.hh:15-186) -- the same fields, methods and ownership rules, so
+// proxy and agent code written against the reference compiles unchanged.
+//
+// One difference, the reason this header exists: allocateData takes buffers
+// of 64 KiB and more from libnxec's pinned host arena (nxec_host_alloc,
+// include/nxec.h §6) instead of posix_memalign/malloc.  They are page
+// aligned (>= the 32 bytes chunk.hh:66 asks for) and device-mapped, so
+// RSCode::encode / CodingUtils::encode give them to the GPU without a staging
+// copy.  release() returns arena buffers to the arena and free()s everything
+// else, so buffers the caller malloc()ed and attached (io.cc:213,
+// container_manager.cc:241) keep working.  Without a usable GPU, or past the
+// arena's bound, allocation falls back to ordinary memory.
+//
+// File uuids are boost::uuids::uuid when boost is available (the Nexoedge
+// build), else a 16-byte value type of the same layout.
 #ifndef NXEC_CODING_CHUNK_HH
 #define NXEC_CODING_CHUNK_HH
 
+#include <openssl/evp.h>
+#include <openssl/md5.h>
+#include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-struct Chunk {
-  int chunkId = -1;
-  unsigned char *data = nullptr;
-  int size = 0;
-  bool freeData = false;
+#include <string>
 
-  Chunk() = default;
+#include "define.hh"
+#include "nxec.h"
+
+#if __has_include(<boost/uuid/uuid.hpp>)
+#include <boost/uuid/uuid.hpp>
+#include <boost/uuid/uuid_generators.hpp>
+#include <boost/uuid/uuid_io.hpp>
+typedef boost::uuids::uuid chunk_uuid_t;
+inline chunk_uuid_t chunk_nil_uuid() { return boost::uuids::nil_uuid(); }
+inline std::string chunk_uuid_str(const chunk_uuid_t &u) { return boost::uuids::to_string(u); }
+#else
+struct chunk_uuid_t {
+  uint8_t data[16];
+  bool operator==(const chunk_uuid_t &o) const { return memcmp(data, o.data, 16) == 0; }
+  bool operator!=(const chunk_uuid_t &o) const { return !(*this == o); }
+};
+inline chunk_uuid_t chunk_nil_uuid() { return chunk_uuid_t{}; }
+inline std::string chunk_uuid_str(const chunk_uuid_t &u) {  // 8-4-4-4-12 hex, as boost prints it
+  char s[37];
+  int p = 0;
+  for (int i = 0; i < 16; i++) {
+    if (i == 4 || i == 6 || i == 8 || i == 10) s[p++] = '-';
+    snprintf(s + p, 3, "%02x", u.data[i]);
+    p += 2;
+  }
+  return std::string(s, 36);
+}
+#endif
+
+// buffers at least this long come from the pinned arena (NXEC_CHUNK_ARENA_MIN
+// overrides; 0 = never)
+inline size_t chunk_arena_min_bytes() {
+  static const size_t v = [] {
+    const char *e = getenv("NXEC_CHUNK_ARENA_MIN");
+    return e ? static_cast<size_t>(strtoull(e, nullptr, 10)) : static_cast<size_t>(64 * 1024);
+  }();
+  return v;
+}
+
+struct Chunk {
+  unsigned char namespaceId;                 /**< namespace id */
+  chunk_uuid_t fuuid;                        /**< file uuid */
+  int chunkId;                               /**< chunk id */
+  unsigned char *data;                       /**< chunk data */
+  int size;                                  /**< chunk size */
+  bool freeData;                             /**< whether to free data upon destruction */
+  int fileVersion;                           /**< file version number */
+  char chunkVersion[CHUNK_VERSION_MAX_LEN];  /**< chunk version number for revert */
+  unsigned char md5[MD5_DIGEST_LENGTH];      /**< chunk md5 checksum */
+
+  Chunk() { reset(); }
   ~Chunk() { release(); }
-  Chunk(const Chunk &o) { copy(o); }
+  // copies are deep and moves transfer the buffer (the reference's explicit
+  // copy() / move() semantics), so std::vector<Chunk> never double-frees
+  Chunk(const Chunk &o) {
+    reset();
+    copy(o);
+  }
   Chunk &operator=(const Chunk &o) {
     if (this != &o) copy(o);
     return *this;
   }
-  Chunk(Chunk &&o) noexcept { move(o); }
+  Chunk(Chunk &&o) noexcept {
+    reset();
+    move(o);
+  }
   Chunk &operator=(Chunk &&o) noexcept {
     if (this != &o) move(o);
     return *this;
   }
 
-  void setChunkId(int id) { chunkId = id; }
-  int getChunkId() const { return chunkId; }
+  void copyMeta(const Chunk &src, bool copySize = true) {
+    setId(src.namespaceId, src.fuuid, src.chunkId);
+    fileVersion = src.fileVersion;
+    strncpy(chunkVersion, src.chunkVersion, CHUNK_VERSION_MAX_LEN);
+    copyMD5(src);
+    if (copySize) size = src.size;
+  }
 
-  // 32-byte aligned allocation when `aligned` (chunk.hh:55-89 semantics)
-  bool allocateData(int n, bool aligned = false) {
-    if (n <= 0) return false;
-    if (data && size == n && freeData && !aligned) return true;
-    unsigned char *p = nullptr;
-    if (aligned) {
-      if (posix_memalign(reinterpret_cast<void **>(&p), 32, n) != 0) p = nullptr;
-    } else {
-      p = static_cast<unsigned char *>(malloc(n));
+  void setId(unsigned char namespaceIdt, chunk_uuid_t uuidt, int chunkIdt) {
+    namespaceId = namespaceIdt;
+    fuuid = uuidt;
+    chunkId = chunkIdt;
+  }
+  void setChunkId(int chunkIdt) { chunkId = chunkIdt; }
+
+  // chunk.hh:55-85: no allocation for sizet <= 0; keep an owned buffer of the
+  // same size unless alignment is requested
+  bool allocateData(int sizet, bool aligned = false) {
+    if (sizet <= 0) return false;
+    if (data != NULL && size == sizet && freeData && !aligned) return true;
+    unsigned char *datat = NULL;
+    const size_t min = chunk_arena_min_bytes();
+    if (min > 0 && static_cast<size_t>(sizet) >= min) {
+      void *p = NULL;
+      if (nxec_host_alloc(static_cast<size_t>(sizet), &p) == NXEC_OK) datat = static_cast<unsigned char *>(p);
     }
-    if (!p) return false;
-    if (freeData) free(data);
-    data = p;
-    size = n;
+    if (datat == NULL) {
+      if (aligned) {
+        if (posix_memalign(reinterpret_cast<void **>(&datat), 32, sizet) != 0) datat = NULL;
+      } else {
+        datat = static_cast<unsigned char *>(malloc(sizet));
+      }
+    }
+    if (datat == NULL) return false;
+    if (freeData) freeBuffer(data);
+    data = datat;
+    size = sizet;
     freeData = true;
     return true;
   }
 
   bool copy(const Chunk &src, bool aligned = false) {
     release();
-    chunkId = src.chunkId;
-    if (src.size <= 0 || !src.data) return true;
+    copyMeta(src);
     if (!allocateData(src.size, aligned)) return false;
     memcpy(data, src.data, size);
     return true;
@@ -58,20 +148,67 @@ struct Chunk {
 
   bool move(Chunk &src) {
     release();
-    chunkId = src.chunkId;
+    copyMeta(src);
     data = src.data;
     size = src.size;
     freeData = src.freeData;
-    src.data = nullptr;
+    src.data = 0;
     src.freeData = false;
     return true;
   }
 
-  void release() {
-    if (freeData) free(data);
-    data = nullptr;
+  unsigned char getNamespaceId() const { return namespaceId; }
+  int getChunkId() const { return chunkId; }
+  chunk_uuid_t getFileUUID() const { return fuuid; }
+  int getFileVersion() const { return fileVersion; }
+  const char *getChunkVersion() const { return chunkVersion; }
+
+  std::string getChunkName() const {
+    return std::to_string(namespaceId) + "_" + chunk_uuid_str(fuuid) + "_" + std::to_string(fileVersion) + "_" +
+           std::to_string(chunkId);
+  }
+
+  // chunk.hh:136-152 (OpenSSL MD5, as MD5Calculator does)
+  bool computeMD5() {
+    if (size <= 0) return false;
+    unsigned int len = MD5_DIGEST_LENGTH;
+    return EVP_Digest(data, static_cast<size_t>(size), md5, &len, EVP_md5(), NULL) == 1;
+  }
+  bool verifyMD5() {
+    unsigned char cur[MD5_DIGEST_LENGTH];
+    unsigned int len = MD5_DIGEST_LENGTH;
+    EVP_Digest(data, static_cast<size_t>(size), cur, &len, EVP_md5(), NULL);
+    return memcmp(md5, cur, MD5_DIGEST_LENGTH) == 0;
+  }
+  void copyMD5(const Chunk &src) { memcpy(md5, src.md5, MD5_DIGEST_LENGTH); }
+
+  // chunk.hh:158-164, kept as is (including its memcmp truthiness)
+  bool matchMeta(const Chunk &in) {
+    return chunkId == in.chunkId && memcmp(md5, in.md5, MD5_DIGEST_LENGTH) && size == in.size;
+  }
+  void resetMD5() { memset(md5, 0, MD5_DIGEST_LENGTH); }
+
+  void reset() {
+    namespaceId = INVALID_NAMESPACE_ID;
+    fuuid = chunk_nil_uuid();
+    chunkId = INVALID_CHUNK_ID;
+    fileVersion = 0;
+    chunkVersion[0] = 0;
+    data = 0;
     size = 0;
-    freeData = false;
+    freeData = true;
+    resetMD5();
+  }
+
+  void release() {
+    if (freeData) freeBuffer(data);
+    reset();
+  }
+
+  static void freeBuffer(unsigned char *p) {
+    if (!p) return;
+    if (nxec_host_arena_owns(p)) nxec_host_free(p);
+    else free(p);
   }
 };
 

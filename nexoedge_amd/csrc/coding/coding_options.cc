@@ -1,7 +1,39 @@
 // See coding_options.hh (reference semantics: coding_options.cc:6-60).
 #include "coding_options.hh"
 
-CodingOptions::CodingOptions() = default;
+#include <atomic>
+#include <cstdint>
+
+namespace {
+// fixed defaults packed in one word (n | k << 8 | car << 16) so a reader never
+// sees a half-updated triple; the provider, when set, takes precedence
+std::atomic<uint32_t> g_fixed{0};
+std::atomic<CodingOptions::DefaultsProvider> g_provider{nullptr};
+}  // namespace
+
+void CodingOptions::setDefaults(coding_param_t n, coding_param_t k, bool car) {
+  g_fixed.store(static_cast<uint32_t>(n) | static_cast<uint32_t>(k) << 8 | (car ? 1u : 0u) << 16,
+                std::memory_order_release);
+}
+
+void CodingOptions::setDefaultsProvider(DefaultsProvider provider) {
+  g_provider.store(provider, std::memory_order_release);
+}
+
+CodingOptions::Defaults CodingOptions::defaults() {
+  if (DefaultsProvider p = g_provider.load(std::memory_order_acquire)) return p();
+  const uint32_t w = g_fixed.load(std::memory_order_acquire);
+  return Defaults{static_cast<coding_param_t>(w & 0xff), static_cast<coding_param_t>((w >> 8) & 0xff),
+                  ((w >> 16) & 1u) != 0};
+}
+
+// coding_options.cc:6-11: the reference reads Config here
+CodingOptions::CodingOptions() {
+  const Defaults d = defaults();
+  _n = d.n;
+  _k = d.k;
+  _car = d.repairUsingCAR;
+}
 CodingOptions::CodingOptions(coding_param_t n, coding_param_t k, bool car) : _n(n), _k(k), _car(car) {}
 CodingOptions::~CodingOptions() = default;
 

@@ -1,7 +1,21 @@
 // Coding parameters (reference: src/common/coding/coding_options.{hh,cc}).
-// The reference constructor pulls n, k and the CAR flag from the Config
-// singleton (coding_options.cc:6-11); here they are constructor arguments,
-// since the INI config lives in the proxy/agent, outside the coding path.
+//
+// The reference's default constructor pulls n, k and the CAR flag out of the
+// Config singleton (coding_options.cc:6-11), and ChunkManager relies on that:
+// it builds its options with the default constructor plus setN/setK
+// (chunk_manager.cc:25-27, :1789-1791), so the CAR flag reaches RSCode only
+// through the constructor.  The coding library cannot link Config (boost INI
+// reader, the whole proxy/agent configuration), so the default constructor
+// reads a process-wide *defaults source* instead:
+//
+//   * a provider function, registered once (integration/config_bridge.cc
+//     registers one that returns Config::getInstance().getN()/getK()/
+//     isRepairUsingCAR(), evaluated at every construction exactly like the
+//     reference), or
+//   * fixed values from setDefaults(), or
+//   * n = k = 0, CAR off when neither was set.
+//
+// Both setters are thread-safe; construction never blocks on them.
 #ifndef NXEC_CODING_OPTIONS_HH
 #define NXEC_CODING_OPTIONS_HH
 
@@ -11,7 +25,14 @@
 
 class CodingOptions {
  public:
-  CodingOptions();
+  struct Defaults {
+    coding_param_t n;
+    coding_param_t k;
+    bool repairUsingCAR;
+  };
+  typedef Defaults (*DefaultsProvider)();
+
+  CodingOptions();  // n, k, CAR from the defaults source (coding_options.cc:6-11)
   CodingOptions(coding_param_t n, coding_param_t k, bool repairUsingCAR = false);
   ~CodingOptions();
 
@@ -22,6 +43,11 @@ class CodingOptions {
   coding_param_t getN();
   coding_param_t getK();
   std::string str(bool withRuntimeOptions = false);
+
+  // ---- process-wide defaults source of the default constructor
+  static void setDefaults(coding_param_t n, coding_param_t k, bool repairUsingCAR);
+  static void setDefaultsProvider(DefaultsProvider provider);  // nullptr: back to setDefaults' values
+  static Defaults defaults();                                  // what CodingOptions() would read now
 
  private:
   coding_param_t _n = 0;

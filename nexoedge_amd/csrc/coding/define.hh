@@ -1,4 +1,4 @@
-// Scalar types of the Nexoedge coding layer (reference: src/common/define.hh:9-19,44-48).
+// Scalar types of the Nexoedge coding layer (reference: src/common/define.hh:9-32,44-48).
 #ifndef NXEC_CODING_DEFINE_HH
 #define NXEC_CODING_DEFINE_HH
 
@@ -11,7 +11,11 @@ typedef uint16_t chunk_id_t;
 typedef uint8_t coding_param_t;
 typedef uint32_t num_t;
 
+typedef unsigned char namespace_id_t;
+
 #define INVALID_CHUNK_ID (int)(-1)
+#define INVALID_NAMESPACE_ID (namespace_id_t)(-1)  // define.hh:28
+#define CHUNK_VERSION_MAX_LEN (unsigned char)(128)  // define.hh:32
 
 // coding schemes known to CodingGenerator (define.hh:44-48)
 enum CodingScheme { RS, UNKNOWN_CODE };

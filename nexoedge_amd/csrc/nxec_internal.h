@@ -69,6 +69,11 @@ LaunchInfo plan_launch(int k, int rows, int64_t vec_count, int64_t nstripes, int
                        bool gather);
 // Enqueues one pass (vector kernel + byte kernel for tails / misaligned data).
 int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream);
+// Zeroes every tile-queue slot of the current device (stream-ordered, then
+// synchronised); for recovery after a device error.
+int reset_work_queues(void *stream);
+// Testing: stores `next_tile` in the counter of the slot the next launch draws.
+int debug_poison_next_queue_slot(uint32_t next_tile);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).
 int prepare_kernels();
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream);

@@ -947,6 +947,31 @@ uint32_t tiles_per_grab(const MulArgs &a) {
 // (4096 launches would have to be in flight at once for two to share one)
 std::atomic<uint32_t> g_next_slot{0};
 
+// A slot is cleaned by the last workgroup of the launch that used it.  A
+// launch that never completes (enqueue failure, aborted stream) would leave a
+// non-zero counter behind, and the launch that draws the same slot 4096
+// launches later would start past tile 0 and silently skip tiles.  Every
+// failed launch therefore zeroes its slot from the host before returning.
+int reset_queue_slots(int first, int count, hipStream_t st) {
+  void *base = nullptr;
+  hipError_t e = hipGetSymbolAddress(&base, HIP_SYMBOL(g_tile_queue));
+  if (e == hipSuccess) {
+    if (count <= 0) {
+      first = 0;
+      count = kQueueSlots;
+    }
+    e = hipMemsetAsync(static_cast<uint8_t *>(base) + static_cast<size_t>(first) * 128, 0,
+                       static_cast<size_t>(count) * 128, st);
+  }
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "tile-queue reset");
+}
+
+int launch_failed(hipError_t e, const char *what, int slot, hipStream_t st) {
+  const int rc = hip_fail(e, what);
+  if (slot >= 0) (void)reset_queue_slots(slot, 1, st);
+  return rc;
+}
+
 // NXEC_TILE_ORDER=static: static tile runs instead of the work queue (A/B probes only)
 bool static_order() {
   const char *env = std::getenv("NXEC_TILE_ORDER");
@@ -983,7 +1008,7 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
       KernelFn fn = li.perm ? kPerm[gather][b.k - 1] : vec_kernel(b.k, li.lds_copies, gather, copy, is_full);
       hipLaunchKernelGGL(fn, dim3(li.grid), dim3(li.block), li.lds_bytes, st, b);
       hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return hip_fail(e, "launch k_mul_vec");
+      if (e != hipSuccess) return launch_failed(e, "launch k_mul_vec", b.queue_slot, st);
     }
   }
   if (a.byte_begin < a.len) {
@@ -996,6 +1021,23 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
     if (e != hipSuccess) return hip_fail(e, "launch k_mul_bytes");
   }
   return NXEC_OK;
+}
+
+int reset_work_queues(void *stream) {
+  const int rc = reset_queue_slots(0, 0, static_cast<hipStream_t>(stream));
+  if (rc) return rc;
+  const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "tile-queue reset sync");
+}
+
+int debug_poison_next_queue_slot(uint32_t next_tile) {
+  void *base = nullptr;
+  hipError_t e = hipGetSymbolAddress(&base, HIP_SYMBOL(g_tile_queue));
+  const uint32_t slot = g_next_slot.load() % kQueueSlots;
+  if (e == hipSuccess)
+    e = hipMemcpy(static_cast<uint8_t *>(base) + static_cast<size_t>(slot) * 128, &next_tile, sizeof(next_tile),
+                  hipMemcpyHostToDevice);
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "tile-queue poison");
 }
 
 int launch_mul_list(int rows, int k, const uint8_t *coeffs, const ListStripe *d_stripes, const int64_t *d_prefix,
@@ -1063,7 +1105,7 @@ int launch_mul_ragged(int rows, int k, const uint8_t *coeffs, const ListStripe *
     hipLaunchKernelGGL(kRagged[k - 1], dim3(static_cast<unsigned>(grid)), dim3(kBlock), ragged_lds(k),
                        static_cast<hipStream_t>(stream), a);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "launch k_mul_ragged");
+    if (e != hipSuccess) return launch_failed(e, "launch k_mul_ragged", a.queue_slot, static_cast<hipStream_t>(stream));
   }
   return NXEC_OK;
 }

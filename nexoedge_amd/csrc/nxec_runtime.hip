@@ -137,6 +137,20 @@ void *host_device_view(const void *h) {
   return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
 }
 
+// Device address of the whole host range [h, h + bytes): both ends must lie in
+// pinned / registered memory of one mapping (the device addresses of the first
+// and last byte differ by bytes - 1), else nullptr -- a buffer registered only
+// in part (hipHostRegister on a sub-range, a frame running past the end of
+// its registration) takes the staged path instead of faulting the GPU.
+void *host_device_view_range(const void *h, size_t bytes) {
+  void *d0 = host_device_view(h);
+  if (!d0 || bytes <= 1) return d0;
+  const void *last = static_cast<const uint8_t *>(h) + (bytes - 1);
+  void *d1 = host_device_view(last);
+  if (!d1 || static_cast<uint8_t *>(d1) - static_cast<uint8_t *>(d0) != static_cast<ptrdiff_t>(bytes - 1)) return nullptr;
+  return d0;
+}
+
 // host entry-point calls in flight (the pipelined, pool-assisted form is for
 // few callers; many concurrent callers are better served one piece each)
 std::atomic<int> g_host_calls{0};
@@ -1014,8 +1028,9 @@ int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char
   // keep more of the link busy than the copy engines do (RS(10,4) 1 MiB,
   // 512 stripes: 71.6 vs 48.7 GiB/s of (k+p)*cs, tools/zero_copy_probe.py).
   {
-    const unsigned char *dd = static_cast<const unsigned char *>(host_device_view(h_data));
-    unsigned char *dp = static_cast<unsigned char *>(host_device_view(h_parity));
+    const unsigned char *dd =
+        static_cast<const unsigned char *>(host_device_view_range(h_data, static_cast<size_t>(nstripes * k * len)));
+    unsigned char *dp = static_cast<unsigned char *>(host_device_view_range(h_parity, static_cast<size_t>(nstripes * p * len)));
     if (dd && dp) {
       std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
       nxec_gf_gen_rs_matrix(enc.data(), n, k);
@@ -1105,16 +1120,11 @@ void frame_copies(const FramePlan &fp, int64_t first, int64_t count, uint8_t *st
   });
 }
 
-// whether every frame is pinned / registered host memory (DMA reads it directly)
-bool frames_pinned(const void *const *frames, int64_t n) {
-  for (int64_t i = 0; i < n; i++) {
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, frames[i]) != hipSuccess) {
-      (void)hipGetLastError();
-      return false;
-    }
-    if (a.type != hipMemoryTypeHost) return false;
-  }
+// whether every frame is pinned / registered host memory over its whole
+// length (DMA reads it directly)
+bool frames_pinned(const void *const *frames, int64_t n, int64_t len) {
+  for (int64_t i = 0; i < n; i++)
+    if (!host_device_view_range(frames[i], static_cast<size_t>(len))) return false;
   return true;
 }
 
@@ -1133,7 +1143,7 @@ int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, in
   if (rc || nchunks == 0 || len == 0) return rc;
   if ((rc = ensure_device(ctx->device))) return rc;
   hipStream_t st = pick_stream(ctx, stream);
-  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks)) {
+  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks, len)) {
     for (int64_t i = 0; i < nchunks; i++)
       NXEC_HIP(hipMemcpyAsync(d_dst + i * dst_stride, h_chunks[i], size_t(len), hipMemcpyHostToDevice, st));
     NXEC_HIP(hipStreamSynchronize(st));
@@ -1183,7 +1193,7 @@ int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src
   if (rc || nchunks == 0 || len == 0) return rc;
   if ((rc = ensure_device(ctx->device))) return rc;
   hipStream_t st = pick_stream(ctx, stream);
-  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks)) {
+  if (len >= kFrameDirect && frames_pinned(reinterpret_cast<const void *const *>(h_chunks), nchunks, len)) {
     for (int64_t i = 0; i < nchunks; i++)
       NXEC_HIP(hipMemcpyAsync(h_chunks[i], d_src + i * src_stride, size_t(len), hipMemcpyDeviceToHost, st));
     NXEC_HIP(hipStreamSynchronize(st));
@@ -1330,7 +1340,7 @@ int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
   for (int64_t s = 0; s < nstripes && direct; s++)
     for (int j = 0; j < w && direct; j++) {
       const int c = j < k ? inputs[j] : failed[j - k];
-      void *dv = host_device_view(frames[s * n + c]);
+      void *dv = host_device_view_range(frames[s * n + c], static_cast<size_t>(len));
       direct = dv != nullptr;
       (j < k ? tab[s * k + j] : tab[nstripes * k + s * e + (j - k)]) = reinterpret_cast<uintptr_t>(dv);
     }
@@ -1468,6 +1478,66 @@ int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *
   return rc;
 }
 
+}  // extern "C"
+
+namespace {
+
+constexpr int kNotPinned = 1;  // encode_host_pinned: some buffer is not device-mapped
+
+// nxec_encode_host on buffers that are all pinned / registered host memory
+// (16-byte aligned, e.g. Chunk buffers from the pinned arena, chunk.hh): the
+// inputs never pass through a host staging copy.  Few concurrent callers: one
+// kernel reads the inputs and writes the outputs over PCIe through device
+// pointer tables (zero copy).  Many callers: the copy engines DMA every input
+// straight from its chunk into HBM and every output straight back, around
+// the kernel (they share the link better than many zero-copy kernels,
+// DESIGN.md §6).  Returns kNotPinned (nothing done) when a buffer is pageable.
+int encode_host_pinned(nxec_ctx_t *ctx, int len, int k, int rows, const unsigned char *coeffs,
+                       const unsigned char *const *data, unsigned char *const *coding, int inflight) {
+  std::vector<uint64_t> tab(static_cast<size_t>(k) + rows);
+  for (int i = 0; i < k + rows; i++) {
+    const void *h = i < k ? static_cast<const void *>(data[i]) : static_cast<const void *>(coding[i - k]);
+    void *dv = aligned16(h) ? host_device_view_range(h, static_cast<size_t>(len)) : nullptr;
+    if (!dv) return kNotPinned;
+    tab[i] = reinterpret_cast<uintptr_t>(dv);
+  }
+  const bool zero_copy = inflight <= 2;
+  const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;
+  const size_t need = zero_copy ? tab.size() * sizeof(uint64_t) : static_cast<size_t>(stride) * (k + rows);
+  Slot *slot = nullptr;
+  int rc = acquire_slot(ctx, need, &slot);
+  if (rc) return rc;
+  hipStream_t st = slot->stream;
+  if (zero_copy) {
+    std::memcpy(slot->h, tab.data(), tab.size() * sizeof(uint64_t));
+    rc = hip_check(hipMemcpyAsync(slot->d, slot->h, tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st),
+                   "pointer table H2D");
+    if (!rc)
+      rc = nxec_stripes_mul_ptrs(ctx, rows, k, coeffs, reinterpret_cast<const unsigned char *const *>(slot->d),
+                                 reinterpret_cast<unsigned char *const *>(slot->d + size_t(k) * sizeof(uint64_t)), len,
+                                 1, st);
+  } else {
+    for (int j = 0; j < k && !rc; j++)
+      rc = hip_check(hipMemcpyAsync(slot->d + j * stride, data[j], size_t(len), hipMemcpyHostToDevice, st), "H2D");
+    std::vector<int32_t> dst(rows);
+    for (int r = 0; r < rows; r++) dst[r] = k + r;
+    if (!rc)
+      rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d, nullptr, stride, 0, slot->d, dst.data(), stride, 0, nullptr,
+                            len, 1, st);
+    for (int r = 0; r < rows && !rc; r++)
+      rc = hip_check(hipMemcpyAsync(coding[r], slot->d + (k + r) * stride, size_t(len), hipMemcpyDeviceToHost, st),
+                     "D2H");
+  }
+  const hipError_t e = hipStreamSynchronize(st);  // the slot goes back only once drained
+  if (!rc) rc = hip_check(e, "encode_host (pinned) sync");
+  release_slot(ctx, slot);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
 int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
                         unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out) {
   int ncopy = 0;
@@ -1480,6 +1550,17 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   nxec_ctx_t *ctx = nullptr;
   int rc = default_ctx(&ctx);
   if (rc) return rc;
+  struct InFlight {
+    int n;
+    InFlight() : n(g_host_calls.fetch_add(1) + 1) {}
+    ~InFlight() { g_host_calls.fetch_sub(1); }
+  } inflight;
+  // chunk buffers that are already pinned (the chunk arena, registered
+  // receive pools): straight to the GPU, no staging memcpy
+  if (ncopy == 0) {
+    rc = encode_host_pinned(ctx, len, k, rows, coeffs, data, coding, inflight.n);
+    if (rc != kNotPinned) return rc;
+  }
   const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;  // keep chunks 16-B aligned in staging
   const int nout = rows + ncopy;
   const int nchunks = k + nout;
@@ -1490,11 +1571,6 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   // pinned staging while the copy engine and the kernel work on piece p-1;
   // outputs come back per piece.  Staging layout [k inputs][rows outputs]
   // [ncopy pass-through outputs], each chunk at a 16-byte stride.
-  struct InFlight {
-    int n;
-    InFlight() : n(g_host_calls.fetch_add(1) + 1) {}
-    ~InFlight() { g_host_calls.fetch_sub(1); }
-  } inflight;
   const int64_t piece = (len >= 2 * kHostPiece && inflight.n <= 2) ? kHostPiece : stride;
   const int npieces = static_cast<int>((len + piece - 1) / piece);
   while (static_cast<int>(slot->events.size()) < npieces) {
@@ -1713,6 +1789,24 @@ int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream) 
   }
   (void)hipFree(d_acc);
   return rc;
+}
+
+int nxec_host_range_mapped(const void *p, size_t bytes) {
+  return p && host_device_view_range(p, bytes) != nullptr ? 1 : 0;
+}
+
+int nxec_reset_work_queues(void) {
+  int dev = 0;
+  NXEC_HIP(hipGetDevice(&dev));
+  int rc = ensure_device(dev);
+  return rc ? rc : reset_work_queues(nullptr);
+}
+
+int nxec_debug_poison_next_queue_slot(uint32_t next_tile) {
+  int dev = 0;
+  NXEC_HIP(hipGetDevice(&dev));
+  int rc = ensure_device(dev);
+  return rc ? rc : debug_poison_next_queue_slot(next_tile);
 }
 
 int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len) {

@@ -87,6 +87,17 @@ def fill_bytes(nbytes: int, seed: int) -> np.ndarray:
     return out
 
 
+_o.orc_fill_bytes_at.argtypes = [vp, C.c_int64, C.c_uint64, C.c_int64]
+
+
+def fill_bytes_at(out: np.ndarray, seed: int, byte_off: int) -> np.ndarray:
+    """Bytes [byte_off, byte_off + out.nbytes) of fill_bytes(., seed) into `out`
+    (byte_off a multiple of 8)."""
+    assert byte_off % 8 == 0 and out.dtype == np.uint8 and out.flags["C_CONTIGUOUS"]
+    _o.orc_fill_bytes_at(_p(out), out.nbytes, C.c_uint64(seed), byte_off // 8)
+    return out
+
+
 def matmul(coeffs: np.ndarray, srcs: Sequence[np.ndarray]) -> List[np.ndarray]:
     c = np.ascontiguousarray(coeffs, dtype=np.uint8)
     rows, k = c.shape
@@ -101,6 +112,27 @@ def matmul(coeffs: np.ndarray, srcs: Sequence[np.ndarray]) -> List[np.ndarray]:
 _o.orc_simd_level.restype = C.c_int
 _o.orc_simd_encode.restype = C.c_int
 _o.orc_simd_encode.argtypes = [C.c_int, C.c_size_t, C.c_int, C.c_int, vp, vp, vp]
+
+
+_o.orc_simd_rscode_encode_range.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp]
+_o.orc_simd_rscode_decode_range.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int64, vp, vp,
+                                            C.c_int, vp, vp]
+
+
+def simd_rscode_encode_range(level: int, n: int, k: int, cs: int, lo: int, hi: int, data: np.ndarray,
+                             chunks: np.ndarray, parity_rows: np.ndarray) -> None:
+    """RSCode::encode (rs.cc:57-92) for stripes [lo, hi): copy data [s][k][cs] into
+    the stripe's chunks [s][n][cs] (rs.cc:80), then SIMD-encode the parity."""
+    pr = np.ascontiguousarray(parity_rows, dtype=np.uint8)
+    _o.orc_simd_rscode_encode_range(level, n, k, cs, lo, hi, _p(data), _p(chunks), _p(pr))
+
+
+def simd_rscode_decode_range(level: int, n: int, k: int, cs: int, lo: int, hi: int, chunks: np.ndarray,
+                             ids: Sequence[int], matrix: np.ndarray, out: np.ndarray) -> None:
+    """rows x k matrix over chunks `ids` of stripes [lo, hi) -> out [s][rows][cs]."""
+    m = np.ascontiguousarray(matrix, dtype=np.uint8)
+    i = np.asarray(list(ids), dtype=np.int32)
+    _o.orc_simd_rscode_decode_range(level, n, k, cs, lo, hi, _p(chunks), _p(i), m.shape[0], _p(m), _p(out))
 
 
 def simd_level() -> int:

@@ -321,6 +321,8 @@ int main(void) {
     for (int ci = 0; ci < 7; ci++) case_encode(main_geo[gi][0], main_geo[gi][1], main_cs[ci], 4096);
   for (int n = 4; n <= 12; n++)
     for (int m = 1; m <= n - 2; m++) { case_encode(n, n - m, 1, 64); case_encode(n, n - m, 31, 4096); case_encode(n, n - m, 1000, 0); }
+  /* config 1, literal sample reading (sample/storage_class.ini:6-9): (n,k)=(4,2), 4 MiB file -> 2 MiB chunks */
+  case_encode(4, 2, 2 << 20, 4096);
   printf("\n]");
 
   /* decode */
@@ -346,6 +348,14 @@ int main(void) {
       for (int i = 0; i < m; i++) f[i] = i;
       case_decode(n, n - m, 1000, f, m, "first");
     }
+  {
+    int f[2] = {0, 1};
+    case_decode(4, 2, 2 << 20, f, 2, "first");
+    int g[2] = {2, 3};
+    case_decode(4, 2, 2 << 20, g, 2, "parity");
+    int h[2] = {1, 3};
+    case_decode(4, 2, 2 << 20, h, 2, "mixed");
+  }
   printf("\n]");
 
   /* repair: every single and double failure for the coding_test pairs; singles for the configs */
@@ -369,6 +379,7 @@ int main(void) {
     case_repair(n, k, 1 << 20, f0, 1);
     case_repair(n, k, 1 << 20, fl, 1);
   }
+  for (int a = 0; a < 4; a++) case_repair(4, 2, 2 << 20, &a, 1); /* config 1, literal (4,2) 2 MiB */
   printf("\n]");
 
   /* CAR repair */

@@ -158,3 +158,40 @@ int orc_simd_encode(int level, size_t len, int k, int rows, const uint8_t *coef,
   }
   return level;
 }
+
+/* ---- the reference's per-stripe coding calls, for bench.py's cpu_baseline ----
+ * One call per host thread over a contiguous stripe range, so the timed loop
+ * runs entirely in C (no interpreter between stripes).
+ *
+ * RSCode::encode (rs.cc:57-92): the k data chunks are copied out of the
+ * caller's [k][cs] stripe buffer into the stripe's own chunk buffers (rs.cc:80)
+ * and the parity is encoded from those copies (rs.cc:89).  Chunk buffers of
+ * stripe s: chunks + s * n * cs, chunk i at + i * cs. */
+void orc_simd_rscode_encode_range(int level, int n, int k, int64_t cs, int64_t lo, int64_t hi, const uint8_t *data,
+                                  uint8_t *chunks, const uint8_t *parity_rows /* (n-k) x k */) {
+  const uint8_t *src[256];
+  uint8_t *dst[256];
+  for (int64_t s = lo; s < hi; s++) {
+    uint8_t *st = chunks + s * n * cs;
+    memcpy(st, data + s * k * cs, (size_t)(k * cs)); /* rs.cc:80, one copy per chunk in the reference */
+    for (int j = 0; j < k; j++) src[j] = st + j * cs;
+    for (int r = 0; r < n - k; r++) dst[r] = st + (k + r) * cs;
+    if (n > k) orc_simd_encode(level, (size_t)cs, k, n - k, parity_rows, src, dst);
+  }
+}
+
+/* rows x k matrix applied to the chunks `ids` of every stripe in [lo, hi):
+ * the repair rows of rs.cc:204-225 (rows = e, recover) or the k x k inverse of
+ * rs.cc:196,228-230 (rows = k, the reference's full-output read decode).
+ * Outputs of stripe s at out + s * rows * cs. */
+void orc_simd_rscode_decode_range(int level, int n, int k, int64_t cs, int64_t lo, int64_t hi, const uint8_t *chunks,
+                                  const int32_t *ids, int rows, const uint8_t *matrix, uint8_t *out) {
+  const uint8_t *src[256];
+  uint8_t *dst[256];
+  for (int64_t s = lo; s < hi; s++) {
+    const uint8_t *st = chunks + s * n * cs;
+    for (int j = 0; j < k; j++) src[j] = st + (int64_t)ids[j] * cs;
+    for (int r = 0; r < rows; r++) dst[r] = out + (s * rows + r) * cs;
+    orc_simd_encode(level, (size_t)cs, k, rows, matrix, src, dst);
+  }
+}

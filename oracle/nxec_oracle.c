@@ -268,6 +268,12 @@ void orc_fill_bytes(uint8_t *p, int64_t nbytes, uint64_t seed) {
   }
 }
 
+/* bytes [word_off*8, word_off*8 + nbytes) of the same stream (the device
+ * fill of a larger buffer, read back piecewise) */
+void orc_fill_bytes_at(uint8_t *p, int64_t nbytes, uint64_t seed, int64_t word_off) {
+  orc_fill_bytes(p, nbytes, seed + (uint64_t)word_off * 0x9E3779B97F4A7C15ull);
+}
+
 struct enc_job {
   int k, rows;
   const uint8_t *a, *src;

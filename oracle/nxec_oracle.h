@@ -71,12 +71,21 @@ void orc_fill_bytes(uint8_t *p, int64_t nbytes, uint64_t seed);
 double orc_time_encode(int k, int rows, const uint8_t *a, const uint8_t *src, uint8_t *dst,
                        int64_t cs, int64_t nstripes, int threads);
 
+/* orc_fill_bytes' stream from 8-byte word `word_off` on */
+void orc_fill_bytes_at(uint8_t *p, int64_t nbytes, uint64_t seed, int64_t word_off);
+
 /* CPU baseline stand-in for ISA-L's SIMD kernels (nxec_cpu_simd.c):
  * split-nibble vpshufb, AVX-512BW (level 512) / AVX2 (256) / scalar (0);
  * level -1 = best available.  Returns the level used. */
 int orc_simd_level(void);
 int orc_simd_encode(int level, size_t len, int k, int rows, const uint8_t *coef, const uint8_t *const *src,
                     uint8_t *const *dst);
+/* the reference's per-stripe calls over a stripe range (bench.py cpu_baseline):
+ * RSCode::encode incl. the rs.cc:80 copy, and a rows x k decode/recover */
+void orc_simd_rscode_encode_range(int level, int n, int k, int64_t cs, int64_t lo, int64_t hi, const uint8_t *data,
+                                  uint8_t *chunks, const uint8_t *parity_rows);
+void orc_simd_rscode_decode_range(int level, int n, int k, int64_t cs, int64_t lo, int64_t hi, const uint8_t *chunks,
+                                  const int32_t *ids, int rows, const uint8_t *matrix, uint8_t *out);
 
 #ifdef __cplusplus
 }

@@ -66,3 +66,31 @@ def test_invalid_arguments_rejected_before_device_use():
     rc = _lib.lib.nxec_rs_encode_stripes(None, 3, 4, None, 0, 0, 16, 1, None)
     assert rc == _lib.NXEC_ERR_INVALID
     assert b"invalid" in _lib.lib.nxec_last_error()
+
+
+def test_status_forms_return_errors_instead_of_aborting():
+    """The ISA-L-signature drop-in has a _status twin that reports bad arguments
+    (and device errors) as return codes; the process keeps running."""
+    import numpy as np
+
+    t = np.zeros(32 * 4, dtype=np.uint8)
+    src = (ctypes.c_void_p * 2)()
+    dst = (ctypes.c_void_p * 2)()
+    tp = ctypes.c_void_p(t.ctypes.data)
+    assert _lib.lib.nxec_ec_encode_data_status(16, 0, 1, tp, src, dst) == _lib.NXEC_ERR_INVALID  # k < 1
+    assert _lib.lib.nxec_ec_encode_data_status(16, 2, 0, tp, src, dst) == _lib.NXEC_ERR_INVALID  # rows < 1
+    assert _lib.lib.nxec_ec_encode_data_status(16, 2, 1, None, src, dst) == _lib.NXEC_ERR_INVALID  # no tables
+    assert _lib.lib.nxec_ec_encode_data_status(-1, 2, 1, tp, src, dst) == _lib.NXEC_ERR_INVALID  # len < 0
+    assert _lib.lib.nxec_encode_host(16, 200, 1, tp, src, dst) == _lib.NXEC_ERR_INVALID  # k > NXEC_MAX_K
+    assert b"invalid" in _lib.lib.nxec_last_error()
+
+
+def test_arena_without_device_falls_back():
+    """nxec_host_alloc reports failure (it never hands out unpinned memory) when
+    no device is usable; Chunk::allocateData then uses ordinary memory."""
+    if nxec.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    p = ctypes.c_void_p()
+    rc = _lib.lib.nxec_host_alloc(1 << 20, ctypes.byref(p))
+    assert rc in (_lib.NXEC_ERR_NODEV, _lib.NXEC_ERR_NOMEM) and not p.value
+    assert _lib.lib.nxec_host_arena_owns(None) == 0

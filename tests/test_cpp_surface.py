@@ -24,8 +24,10 @@ def test_surface_binary_built():
 
 
 @pytest.mark.gpu
-def test_rscode_surface_matches_reference(golden):
-    cs = 1000
+@pytest.mark.parametrize("cs", [1000, 65537])
+def test_rscode_surface_matches_reference(golden, cs):
+    """cs = 65537: the chunks RSCode::encode allocates come from the pinned
+    arena (Chunk::allocateData >= 64 KiB), so encode runs the no-staging path."""
     r = subprocess.run([BIN, str(cs)], capture_output=True, text=True, timeout=600)
     out = r.stdout.splitlines()
     fails = [l for l in out if l.startswith("FAIL")]
@@ -65,6 +67,73 @@ def test_rscode_surface_matches_reference(golden):
     # 2 CAR modes x (54 coding_test pairs + 3 config geometries)
     assert checked["ENC"] == 2 * 57 and checked["DEC"] == 2 * 57
     assert checked["REP"] > 500 and checked["RP2"] > 2000
+
+
+FLOW = os.path.join(ROOT, "build", "chunk_manager_flow_test")
+
+
+def _flow(cases, timeout=300):
+    args = [str(v) for c in cases for v in c]
+    r = subprocess.run([FLOW] + args, capture_output=True, text=True, timeout=timeout)
+    blocks, cur = [], None
+    for line in r.stdout.splitlines():
+        f = line.split()
+        if not f:
+            continue
+        if f[0] == "CASE":
+            cur = {"case": tuple(int(x) for x in f[1:]), "part": []}
+            blocks.append(cur)
+        elif cur is not None and f[0] == "PART":
+            cur["part"].append(f[2])
+        elif cur is not None and f[0] in ("ENC", "FINAL", "MATCH", "REFUSED_WITHOUT_CAR"):
+            cur[f[0]] = f[1]
+        elif cur is not None and f[0] == "OPTIONS":
+            cur["OPTIONS"] = f[1:]
+    return r, blocks
+
+
+def test_default_options_read_config_via_bridge():
+    """CodingOptions() + setN/setK, as ChunkManager builds them
+    (chunk_manager.cc:25-27, 1789-1791), carries Config's CAR flag through the
+    bridge (CPU: the options line is printed before any GPU call)."""
+    assert os.path.exists(FLOW), "run `make` (build/chunk_manager_flow_test)"
+    for car in (1, 0):
+        _, blocks = _flow([(16, 12, 1000, 0, 4, car, 1)], timeout=60)
+        assert blocks and blocks[0]["OPTIONS"] == [f"16-12{car}", f"16-12{car}"], blocks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("at_proxy", [1, 0])
+def test_unmodified_chunk_manager_car_repair(golden, at_proxy):
+    """CAR single-failure repair with CAR taken from Config only (no setRepairUsingCAR
+    call, as in the reference), at the proxy (accessGroupedChunks + RSCode::decode
+    with G < k partials, chunk_manager.cc:1029,1141) and at an agent
+    (RPR_CHUNK_REQ, agent.cc:249-339): partials and result equal the golden CAR cases."""
+    cases = [(c["n"], c["k"], c["cs"], c["failed"], c["rack_size"], 1, at_proxy) for c in golden["car"]]
+    r, blocks = _flow(cases)
+    assert r.returncode == 0 and len(blocks) == len(cases), (r.stdout[-3000:], r.stderr[-2000:])
+    for c, b in zip(golden["car"], blocks):
+        assert b["MATCH"] == "1", b
+        assert b["part"] == list(c["partials_sha256"]), (c, b)
+        assert b["FINAL"] == c["final_sha256"], (c, b)
+        enc = [e["parity_sha256"] for e in golden["encode"] if (e["n"], e["k"], e["cs"]) == (c["n"], c["k"], c["cs"])]
+        if enc:
+            assert b["ENC"] == enc[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("at_proxy", [1, 0])
+def test_unmodified_chunk_manager_conventional_repair(golden, at_proxy):
+    """Same flows with repair_using_car = 0: k inputs and the plan's repair row,
+    at the proxy (RSCode::decode) and at an agent (CodingUtils::encode with the
+    proxy's matrix, agent.cc:339); fewer than k inputs are refused (rs.cc:133-136)."""
+    cases = [(c["n"], c["k"], c["cs"], c["failed"], c["rack_size"], 0, at_proxy) for c in golden["car"]]
+    r, blocks = _flow(cases)
+    assert r.returncode == 0 and len(blocks) == len(cases), (r.stdout[-3000:], r.stderr[-2000:])
+    for c, b in zip(golden["car"], blocks):
+        assert b["MATCH"] == "1" and b["FINAL"] == c["final_sha256"], (c, b)
+        if at_proxy:
+            assert b["REFUSED_WITHOUT_CAR"] == "1", b
 
 
 COMPAT = os.path.join(ROOT, "build", "isal_compat_test")

@@ -95,3 +95,32 @@ def test_gloo_world2_reduction(tmp_path):
     lines = sorted(l for o, _ in outs for l in o.splitlines() if l.startswith("rank="))
     assert lines[0] == "rank=0 world=2 lo=0 hi=2048 max=0.020 total=4096"
     assert lines[1] == "rank=1 world=2 lo=2048 hi=4096 max=0.020 total=4096"
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = dict(os.environ, **(env_extra or {}))
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_launches_ranks_itself():
+    """`bench.py --gpus N` without torch.distributed.run starts N rank
+    processes (gloo rendezvous on 127.0.0.1) and prints rank 0's single line
+    with n_gpus = N (dry run: no GPU work)."""
+    import json
+
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
+    assert abs(d["max_elapsed_s"] - 0.002) < 1e-9  # max over ranks, not rank 0's own value
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    r = _bench(["--gpus", "2", "--dry-run"], {"NXEC_DRY_RUN_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert "rank 1 exited with status 3" in r.stderr
