@@ -69,6 +69,38 @@ tools/microbench/chunk_stride: tools/microbench/chunk_stride.hip $(LIBDIR)/libnx
 tools/microbench/lut_variants: tools/microbench/lut_variants.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 $< -o $@
 
+# ---- sanitizer builds of the host code (CPU only; SURVEY §5, reference
+# CMakeLists.txt:37-39).  Every source is compiled with the sanitizer on the
+# host side only (-Xarch_host; the device code is the normal gfx950 build and
+# these builds never launch a kernel: they run where no GPU is visible), then
+# tests/cpp/host_sanity_test.cc drives planning, argument
+# validation, the CodingOptions defaults source, Chunk/arena ownership and the
+# host worker pool from 8 threads.  `make sanitize` builds and runs all three.
+SAN_ASAN  := -Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer
+SAN_UBSAN := -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined
+SAN_TSAN  := -Xarch_host -fsanitize=thread
+SAN_CFLAGS = --offload-arch=$(ARCH) -O1 -g -fPIC $(CXXSTD) -Iinclude -I$(CSRC) \
+             -mllvm -amdgpu-atomic-optimizer-strategy=None
+SAN_SRCS := $(LIB_SRCS)
+define SAN_RULES
+build/san/$(1)/obj/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p $$(dir $$@)
+	$(HIPCC) $(SAN_CFLAGS) $(2) -c $$< -o $$@
+build/san/$(1)/libnxec.so: $(patsubst $(CSRC)/%,build/san/$(1)/obj/%.o,$(SAN_SRCS))
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(2) $$^ -o $$@
+build/san/$(1)/host_sanity_test: tests/cpp/host_sanity_test.cc build/san/$(1)/libnxec.so $(HDRS)
+	$(HIPCC) -O1 -g $(CXXSTD) $(2) -Iinclude -I$(CSRC) $$< -Lbuild/san/$(1) -lnxec \
+	    -Wl,-rpath,'$$$$ORIGIN' -lcrypto -lpthread -o $$@
+$(1): build/san/$(1)/host_sanity_test
+endef
+$(eval $(call SAN_RULES,asan,$(SAN_ASAN)))
+$(eval $(call SAN_RULES,ubsan,$(SAN_UBSAN)))
+$(eval $(call SAN_RULES,tsan,$(SAN_TSAN)))
+sanitize: asan ubsan tsan
+	ASAN_OPTIONS=detect_leaks=1 LSAN_OPTIONS=suppressions=tests/cpp/lsan.supp build/san/asan/host_sanity_test
+	UBSAN_OPTIONS=print_stacktrace=1 build/san/ubsan/host_sanity_test
+	TSAN_OPTIONS=ignore_noninstrumented_modules=1 build/san/tsan/host_sanity_test
+
 ref:
 	bash oracle/build_ref.sh
 
@@ -78,4 +110,4 @@ golden: ref
 clean:
 	rm -rf build $(LIBDIR)/libnxec.so oracle/liboracle.so
 
-.PHONY: all ref golden clean tune tools
+.PHONY: all ref golden clean tune tools asan ubsan tsan sanitize

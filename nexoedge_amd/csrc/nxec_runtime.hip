@@ -1482,54 +1482,78 @@ int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *
 
 namespace {
 
-constexpr int kNotPinned = 1;  // encode_host_pinned: some buffer is not device-mapped
+constexpr int kNotPinned = 1;  // encode_host_pinned: some input is not device-mapped
 
-// nxec_encode_host on buffers that are all pinned / registered host memory
-// (16-byte aligned, e.g. Chunk buffers from the pinned arena, chunk.hh): the
-// inputs never pass through a host staging copy.  Few concurrent callers: one
+// nxec_encode_host whose inputs are all pinned / registered host memory
+// (e.g. Chunk buffers from the pinned arena, chunk.hh): the inputs never pass
+// through a host staging copy.  Outputs that are pinned too are written in
+// place; pageable outputs (RSCode::decode's malloc'd result, rs.cc:164-173)
+// come back through the call's pinned slot.  Few concurrent callers: one
 // kernel reads the inputs and writes the outputs over PCIe through device
 // pointer tables (zero copy).  Many callers: the copy engines DMA every input
-// straight from its chunk into HBM and every output straight back, around
-// the kernel (they share the link better than many zero-copy kernels,
-// DESIGN.md §6).  Returns kNotPinned (nothing done) when a buffer is pageable.
+// straight from its chunk into HBM and every output back, around the kernel
+// (they share the link better than many zero-copy kernels).
+// Returns kNotPinned (nothing done) when an input is pageable.
 int encode_host_pinned(nxec_ctx_t *ctx, int len, int k, int rows, const unsigned char *coeffs,
                        const unsigned char *const *data, unsigned char *const *coding, int inflight) {
   std::vector<uint64_t> tab(static_cast<size_t>(k) + rows);
-  for (int i = 0; i < k + rows; i++) {
-    const void *h = i < k ? static_cast<const void *>(data[i]) : static_cast<const void *>(coding[i - k]);
-    void *dv = aligned16(h) ? host_device_view_range(h, static_cast<size_t>(len)) : nullptr;
+  std::vector<bool> out_mapped(rows);
+  for (int j = 0; j < k; j++) {
+    void *dv = aligned16(data[j]) ? host_device_view_range(data[j], static_cast<size_t>(len)) : nullptr;
     if (!dv) return kNotPinned;
-    tab[i] = reinterpret_cast<uintptr_t>(dv);
+    tab[j] = reinterpret_cast<uintptr_t>(dv);
+  }
+  int staged = 0;
+  for (int r = 0; r < rows; r++) {
+    void *dv = aligned16(coding[r]) ? host_device_view_range(coding[r], static_cast<size_t>(len)) : nullptr;
+    out_mapped[r] = dv != nullptr;
+    tab[k + r] = reinterpret_cast<uintptr_t>(dv);
+    staged += dv == nullptr;
   }
   const bool zero_copy = inflight <= 2;
   const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;
-  const size_t need = zero_copy ? tab.size() * sizeof(uint64_t) : static_cast<size_t>(stride) * (k + rows);
+  const size_t tab_bytes = (tab.size() * sizeof(uint64_t) + 4095) / 4096 * 4096;
+  // slot: [pointer table][k + rows chunk slots]; host side holds staged outputs
+  // at the same chunk offsets, device side the DMA'd chunks
+  const size_t need = tab_bytes + static_cast<size_t>(stride) * (k + rows);
   Slot *slot = nullptr;
   int rc = acquire_slot(ctx, need, &slot);
   if (rc) return rc;
   hipStream_t st = slot->stream;
+  auto chunk_off = [&](int i) { return tab_bytes + static_cast<size_t>(stride) * i; };
   if (zero_copy) {
-    std::memcpy(slot->h, tab.data(), tab.size() * sizeof(uint64_t));
-    rc = hip_check(hipMemcpyAsync(slot->d, slot->h, tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st),
-                   "pointer table H2D");
+    uint8_t *hv = staged ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
+    if (staged && !hv) rc = set_error(NXEC_ERR_HIP, "encode_host: staging slot is not device-mapped");
+    for (int r = 0; r < rows && !rc; r++)
+      if (!out_mapped[r]) tab[k + r] = reinterpret_cast<uintptr_t>(hv + chunk_off(k + r));
+    if (!rc) {
+      std::memcpy(slot->h, tab.data(), tab.size() * sizeof(uint64_t));
+      rc = hip_check(hipMemcpyAsync(slot->d, slot->h, tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st),
+                     "pointer table H2D");
+    }
     if (!rc)
       rc = nxec_stripes_mul_ptrs(ctx, rows, k, coeffs, reinterpret_cast<const unsigned char *const *>(slot->d),
                                  reinterpret_cast<unsigned char *const *>(slot->d + size_t(k) * sizeof(uint64_t)), len,
                                  1, st);
   } else {
     for (int j = 0; j < k && !rc; j++)
-      rc = hip_check(hipMemcpyAsync(slot->d + j * stride, data[j], size_t(len), hipMemcpyHostToDevice, st), "H2D");
+      rc = hip_check(hipMemcpyAsync(slot->d + chunk_off(j), data[j], size_t(len), hipMemcpyHostToDevice, st), "H2D");
     std::vector<int32_t> dst(rows);
     for (int r = 0; r < rows; r++) dst[r] = k + r;
     if (!rc)
-      rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d, nullptr, stride, 0, slot->d, dst.data(), stride, 0, nullptr,
-                            len, 1, st);
+      rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d + tab_bytes, nullptr, stride, 0, slot->d + tab_bytes,
+                            dst.data(), stride, 0, nullptr, len, 1, st);
     for (int r = 0; r < rows && !rc; r++)
-      rc = hip_check(hipMemcpyAsync(coding[r], slot->d + (k + r) * stride, size_t(len), hipMemcpyDeviceToHost, st),
+      rc = hip_check(hipMemcpyAsync(out_mapped[r] ? coding[r] : slot->h + chunk_off(k + r),
+                                    slot->d + chunk_off(k + r), size_t(len), hipMemcpyDeviceToHost, st),
                      "D2H");
   }
   const hipError_t e = hipStreamSynchronize(st);  // the slot goes back only once drained
   if (!rc) rc = hip_check(e, "encode_host (pinned) sync");
+  if (!rc && staged)
+    host_parallel_for(rows, [&](int r) {
+      if (!out_mapped[r]) std::memcpy(coding[r], slot->h + chunk_off(k + r), size_t(len));
+    });
   release_slot(ctx, slot);
   return rc;
 }

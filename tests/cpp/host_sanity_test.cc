@@ -1,0 +1,178 @@
+// Host-side sanity driver for the sanitizer builds (make asan / ubsan / tsan,
+// SURVEY §5 "race detection / sanitizers"; the reference keeps ASan flags in
+// CMakeLists.txt:37-39).  Runs without a GPU against a host-only build of
+// libnxec (device code not compiled, --cuda-host-only): every path here is
+// host code -- GF(2^8) planning (gf_host.cpp), argument validation of every
+// entry point, the CodingOptions defaults source, Chunk ownership with the
+// pinned arena falling back to malloc, RSCode's host copies through the
+// worker pool, all under concurrency.  Compute entry points must fail with
+// NXEC_ERR_NODEV (or INVALID) and never crash, leak or race.
+//
+// Exit 0 iff every check passed.
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "coding/coding_generator.hh"
+#include "coding/coding_util.hh"
+#include "nxec.h"
+
+static std::atomic<int> g_fail{0};
+#define CHECK(cond, ...)            \
+  do {                              \
+    if (!(cond)) {                  \
+      std::printf("FAIL ");         \
+      std::printf(__VA_ARGS__);     \
+      std::printf("\n");            \
+      g_fail++;                     \
+    }                               \
+  } while (0)
+
+static void gf_and_planning() {
+  for (int a = 0; a < 256; a++) {
+    CHECK(nxec_gf_mul(a, 1) == a, "mul by 1");
+    if (a) CHECK(nxec_gf_mul(a, nxec_gf_inv(a)) == 1, "inverse %d", a);
+  }
+  std::mt19937 rng(7);
+  std::vector<unsigned char> enc(NXEC_MAX_N * NXEC_MAX_K), rm(NXEC_MAX_N * NXEC_MAX_K);
+  for (int n = 2; n <= NXEC_MAX_N; n += (n < 24 ? 1 : 13)) {
+    for (int k = 1; k <= n && k <= NXEC_MAX_K; k += (k < 20 ? 1 : 17)) {
+      nxec_gen_rs_matrix(enc.data(), n, k);
+      std::vector<int32_t> ids(n);
+      int ni = 0, mi = 0;
+      const int maxf = std::min(n - k, 4);
+      for (int nf = 0; nf <= maxf; nf++) {
+        std::vector<int32_t> f;
+        for (int c = 0; c < n && static_cast<int>(f.size()) < nf; c++)
+          if (rng() % 3 == 0 || n - c <= nf - static_cast<int>(f.size())) f.push_back(c);
+        int rc = nxec_rs_plan(n, k, f.data(), nf, 1, ids.data(), &ni, &mi, rm.data());
+        // the Vandermonde-derived matrix is only guaranteed invertible in ISA-L's
+        // documented range; elsewhere -1 (singular) is a valid answer
+        CHECK(rc == NXEC_OK || rc == NXEC_ERR_SINGULAR, "plan (%d,%d) nf=%d rc=%d", n, k, nf, rc);
+        if (rc == NXEC_OK) CHECK(ni == n - nf && mi == k, "plan sizes");
+      }
+      std::vector<int32_t> tooMany(n - k + 1);
+      for (int i = 0; i <= n - k; i++) tooMany[i] = i;
+      CHECK(nxec_rs_plan(n, k, tooMany.data(), n - k + 1, 1, ids.data(), &ni, &mi, rm.data()) == NXEC_ERR_INVALID,
+            "too many failures rejected (%d,%d)", n, k);
+    }
+  }
+  // CAR grouping (chunk_manager.cc:929-986) with racks of 4
+  const int n = 16, k = 12;
+  std::vector<int32_t> go, gc;
+  for (int c = 0; c < n; c++) {
+    if (c % 4 == 0) go.push_back(static_cast<int32_t>(gc.size()));
+    gc.push_back(c);
+  }
+  go.push_back(static_cast<int32_t>(gc.size()));
+  for (int f = 0; f < n; f++) {
+    std::vector<int32_t> so(go.size() + 1), sc(k);
+    std::vector<unsigned char> cf(k);
+    int ns = 0;
+    CHECK(nxec_car_plan(n, k, f, go.data(), gc.data(), static_cast<int>(go.size()) - 1, so.data(), sc.data(),
+                        cf.data(), &ns) == NXEC_OK && ns >= 1,
+          "car plan f=%d", f);
+  }
+  int64_t a = 0, b = 0, c = 0;
+  CHECK(nxec_object_layout(14, 10, 0, 1 << 20, &a, &b, &c) == NXEC_OK && a == 0, "empty object");
+  CHECK(nxec_object_layout(14, 10, (int64_t(1) << 40) + 7, 1 << 20, &a, &b, &c) == NXEC_OK && a == b + 1,
+        "1 TiB object");
+  CHECK(nxec_object_layout(14, 10, 5, 0, &a, &b, &c) == NXEC_ERR_INVALID, "zero chunk size rejected");
+}
+
+static void argument_validation() {
+  unsigned char coef[4] = {1, 2, 3, 4}, buf[64] = {0};
+  const unsigned char *src[2] = {buf, buf + 16};
+  unsigned char *dst[2] = {buf + 32, buf + 48};
+  CHECK(nxec_encode_host(16, 0, 1, coef, src, dst) == NXEC_ERR_INVALID, "k=0");
+  CHECK(nxec_encode_host(-5, 2, 1, coef, src, dst) == NXEC_ERR_INVALID, "len<0");
+  CHECK(nxec_encode_host(16, 2, 1, nullptr, src, dst) == NXEC_ERR_INVALID, "null coeffs");
+  CHECK(nxec_ec_encode_data_status(16, 2, 1, nullptr, src, dst) == NXEC_ERR_INVALID, "null tables");
+  const int rc = nxec_encode_host(16, 2, 1, coef, src, dst);
+  CHECK(rc == NXEC_ERR_NODEV || rc == NXEC_ERR_HIP, "no device -> error, got %d", rc);
+  nxec_ctx_t *ctx = nullptr;
+  CHECK(nxec_ctx_create(0, &ctx) != NXEC_OK && ctx == nullptr, "no context without a device");
+  CHECK(nxec_stripes_mul(nullptr, 1, 2, coef, buf, nullptr, 16, 32, buf, nullptr, 16, 32, nullptr, 16, 1, nullptr) ==
+            NXEC_ERR_INVALID,
+        "null ctx");
+  CHECK(nxec_rs_encode_stripes(nullptr, 3, 4, buf, 16, 64, 16, 1, nullptr) == NXEC_ERR_INVALID, "n<k");
+  CHECK(nxec_md5_chunks(nullptr, buf, 16, 64, 2, 16, 1, buf, nullptr) == NXEC_ERR_INVALID, "md5 null ctx");
+  CHECK(nxec_agent_encode_batch(nullptr, nullptr, 1, 16, 0) == NXEC_ERR_INVALID, "agent null");
+  CHECK(nxec_gather_chunks(nullptr, nullptr, 1, 16, buf, 16, nullptr) == NXEC_ERR_INVALID, "gather null");
+  nxec_request_t *req = nullptr;
+  CHECK(nxec_gather_chunks_async(nullptr, nullptr, 1, 16, buf, 16, nullptr, &req) == NXEC_ERR_INVALID && !req,
+        "async gather null");
+  CHECK(nxec_request_wait(nullptr) == NXEC_OK, "wait(NULL)");
+  CHECK(nxec_host_range_mapped(buf, sizeof(buf)) == 0, "stack memory is not mapped");
+  void *p = nullptr;
+  const int arc = nxec_host_alloc(1 << 20, &p);
+  CHECK(arc != NXEC_OK && p == nullptr, "arena without device");
+  CHECK(nxec_host_free(buf) == NXEC_ERR_INVALID, "free of a foreign pointer rejected");
+  CHECK(nxec_host_arena_owns(buf) == 0, "foreign pointer not owned");
+}
+
+static void surface(int tid) {
+  // CodingOptions defaults source (coding_options.hh) raced by setters
+  CodingOptions::setDefaults(static_cast<coding_param_t>(14), static_cast<coding_param_t>(10), tid % 2 == 0);
+  for (int i = 0; i < 200; i++) {
+    CodingOptions o;
+    const coding_param_t n = o.getN(), k = o.getK();
+    CHECK((n == 14 && k == 10) || (n == 16 && k == 12), "torn defaults %d-%d", n, k);
+    if (i % 50 == 0) CodingOptions::setDefaults(16, 12, true);
+  }
+  CodingOptions opt(14, 10, false);
+  Coding *code = CodingGenerator::genCoding(CodingScheme::RS, opt);
+  CHECK(code != nullptr, "genCoding");
+  CodingOptions bad(4, 6, false);
+  CHECK(CodingGenerator::genCoding(CodingScheme::RS, bad) == nullptr, "bad params rejected");
+  if (!code) return;
+  const int cs = 65536 + tid;
+  std::vector<unsigned char> data(static_cast<size_t>(10) * cs, static_cast<unsigned char>(tid));
+  std::vector<Chunk> stripe;
+  // the host copy of rs.cc:80 runs on the worker pool, then the GPU call fails
+  CHECK(!code->encode(data.data(), static_cast<length_t>(data.size()), stripe, nullptr), "encode without device");
+  DecodingPlan plan;
+  for (int f = 0; f < 14; f++) {
+    plan.release();
+    std::vector<chunk_id_t> failed{static_cast<chunk_id_t>(f)};
+    CHECK(code->preDecode(failed, plan, nullptr, true), "preDecode %d", f);
+    CHECK(plan.getRepairMatrixSize() == 10, "repair matrix size");
+  }
+  std::vector<chunk_id_t> five{0, 1, 2, 3, 4};
+  CHECK(!code->preDecode(five, plan, nullptr, true), "5 failures rejected");
+  // fewer than k inputs without CAR: refused (rs.cc:133-136), nothing leaks
+  std::vector<Chunk> in(3);
+  for (int i = 0; i < 3; i++) {
+    CHECK(in[i].allocateData(cs, true), "allocateData");
+    in[i].setChunkId(i);
+    std::memset(in[i].data, i, cs);
+  }
+  unsigned char *out = nullptr;
+  length_t osz = 0;
+  CHECK(!code->decode(in, &out, osz, plan, nullptr), "insufficient inputs refused");
+  CHECK(out == nullptr, "no buffer on refusal");
+  // Chunk ownership: copies are deep, moves transfer
+  Chunk c1;
+  CHECK(c1.copy(in[0]) && c1.data != in[0].data && std::memcmp(c1.data, in[0].data, cs) == 0, "deep copy");
+  Chunk c2(std::move(c1));
+  CHECK(c1.data == nullptr && c2.size == cs, "move");
+  std::vector<Chunk> v;
+  for (int i = 0; i < 8; i++) v.push_back(c2);
+  CHECK(c2.computeMD5() && c2.verifyMD5(), "md5");
+  delete code;
+}
+
+int main() {
+  gf_and_planning();
+  argument_validation();
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; t++) th.emplace_back(surface, t);
+  for (auto &t : th) t.join();
+  std::printf("%s %d failures\n", g_fail ? "FAILED" : "PASSED", g_fail.load());
+  return g_fail ? 1 : 0;
+}

@@ -54,14 +54,17 @@ def test_arena_blocks_pinned_recycled_and_owned(gpu_ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("outputs", ["pinned", "pageable"])
 @pytest.mark.parametrize("threads,cs", [(1, 1 << 20), (1, 65536 + 3), (6, 1 << 20), (6, 300001)])
-def test_arena_chunks_encode_without_staging(gpu_ctx, threads, cs):
+def test_arena_chunks_encode_without_staging(gpu_ctx, threads, cs, outputs):
     """RS(10,4) encode of arena chunk buffers through nxec_encode_host (the call
-    under RSCode::encode): one caller runs the zero-copy kernel on the chunks
-    themselves, many callers DMA them; both bit-exact vs the oracle."""
+    under RSCode::encode / RSCode::decode): one caller runs the zero-copy kernel
+    on the chunks themselves, many callers DMA them; pageable outputs (decode's
+    malloc'd result) come back through the staging slot.  Bit-exact vs the oracle."""
     n, k = 14, 10
     enc = nxec.gen_rs_matrix(n, k)[k:]
     blocks = [[arena_alloc(cs) for _ in range(n)] for _ in range(threads)]
+    host_out = [[np.full(cs, 0xEE, dtype=np.uint8) for _ in range(n - k)] for _ in range(threads)]
     want, errors = [], []
     for t in range(threads):
         data = fill_bytes(k * cs, 9100 + t).reshape(k, cs)
@@ -71,10 +74,13 @@ def test_arena_chunks_encode_without_staging(gpu_ctx, threads, cs):
             as_array(blocks[t][k + r], cs)[:] = 0xEE
         want.append(np.stack(oracle.matmul(enc, list(data))))
 
+    def outs(t):
+        return blocks[t][k:] if outputs == "pinned" else [o.ctypes.data for o in host_out[t]]
+
     def work(t):
         try:
             for _ in range(3):
-                encode_ptrs(enc, blocks[t][:k], blocks[t][k:], cs)
+                encode_ptrs(enc, blocks[t][:k], outs(t), cs)
         except Exception as e:  # noqa: BLE001
             errors.append(e)
 
@@ -83,7 +89,10 @@ def test_arena_chunks_encode_without_staging(gpu_ctx, threads, cs):
     [x.join() for x in th]
     assert not errors, errors
     for t in range(threads):
-        got = np.stack([as_array(blocks[t][k + r], cs).copy() for r in range(n - k)])
+        if outputs == "pinned":
+            got = np.stack([as_array(blocks[t][k + r], cs).copy() for r in range(n - k)])
+        else:
+            got = np.stack(host_out[t])
         assert np.array_equal(got, want[t]), t
         for b in blocks[t]:
             lib.nxec_host_free(C.c_void_p(b))

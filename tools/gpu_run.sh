@@ -41,13 +41,18 @@ if has prof; then
   find $OUT/prof -name "*stats*"
 fi
 if has pmc; then
+  # PMC_SETS: ";"-separated "tag:bench args" (default: the headline workload)
   export TMPDIR=/tmp
-  for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$c -o run -- \
-      python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-host-inclusive ${PROF_ARGS:-} \
-      > $OUT/pmc_$c.json 2> $OUT/pmc_$c.err || stop pmc_$c $?
+  IFS=';' read -ra SETS <<< "${PMC_SETS:-rs10_4:--steps 2 --warmup 0}"
+  for set in "${SETS[@]}"; do
+    tag=${set%%:*}; args=${set#*:}
+    for c in FETCH_SIZE WRITE_SIZE; do
+      timeout -s KILL 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_${tag}_$c -o run -- \
+        python3 bench.py --no-cpu-baseline --no-host-inclusive $args \
+        > $OUT/pmc_${tag}_$c.json 2> $OUT/pmc_${tag}_$c.err || stop pmc_${tag}_$c $?
+    done
+    echo "pmc $tag done"
   done
-  echo pmc done
 fi
 if has dropin; then
   timeout -k 10 300 ./build/dropin_rate ${DROPIN_ARGS:-} > $OUT/dropin.jsonl 2> $OUT/dropin.err || stop dropin $?
