@@ -13,11 +13,12 @@ OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip \
             $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp \
-            $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc
+            $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(wildcard $(CSRC)/coding/*.hh)
 
-all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test
+all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test \
+     build/stripe_batch_test
 
 # rs.cc's ISA-L call sequence compiled against include/nxec_isal_compat.h (plain C)
 build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h $(LIBDIR)/libnxec.so
@@ -26,6 +27,11 @@ build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h 
 
 # C++ surface test (reference coding_test.cc flows through RSCode on the GPU)
 build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
+
+# batched ChunkManager entry vs the per-stripe RSCode path
+build/stripe_batch_test: tests/cpp/stripe_batch_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
 
