@@ -87,37 +87,47 @@ int main(int argc, char **argv) {
       std::fflush(stdout);
     }
   }
-  // agent service: one nxec_agent_encode_batch call per 64
-  // ENC_CHUNK_REQ partial encodes (4 local chunks x 1 coefficient row ->
-  // 1 chunk + MD5, container_manager.cc:251, agent.cc:342); bytes = inputs + outputs
+  // agent service: nxec_agent_encode_batch calls of 64
+  // ENC_CHUNK_REQ partial encodes each (4 local chunks x 1 coefficient row ->
+  // 1 chunk + MD5, container_manager.cc:251, agent.cc:342) from 1, 4 and 16
+  // concurrent agent worker threads on one context; bytes = inputs + outputs
   {
     nxec_ctx_t *ctx = nullptr;
     if (nxec_ctx_create(0, &ctx) == NXEC_OK) {
       const int nreq = 64, ni = 4;
-      std::vector<uint8_t> in(static_cast<size_t>(nreq) * ni * cs), out(static_cast<size_t>(nreq) * cs),
-          md5(static_cast<size_t>(nreq) * 16);
-      fill(in.data(), in.size(), 5);
       const uint8_t row[4] = {0x1d, 0x3a, 0x74, 0xe8};
-      std::vector<const unsigned char *> ip(static_cast<size_t>(nreq) * ni);
-      std::vector<unsigned char *> op(nreq);
-      std::vector<nxec_agent_req> reqs(nreq);
-      for (int r = 0; r < nreq; r++) {
-        for (int j = 0; j < ni; j++) ip[r * ni + j] = in.data() + (static_cast<size_t>(r) * ni + j) * cs;
-        op[r] = out.data() + static_cast<size_t>(r) * cs;
-        reqs[r] = {ni, 1, row, ip.data() + r * ni, op.data() + r, md5.data() + r * 16};
+      for (int threads : {1, 4, 16}) {
+        std::atomic<long> calls{0};
+        std::atomic<bool> ok{true};
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> pool;
+        for (int t = 0; t < threads; t++)
+          pool.emplace_back([&, t] {
+            std::vector<uint8_t> in(static_cast<size_t>(nreq) * ni * cs), out(static_cast<size_t>(nreq) * cs),
+                md5(static_cast<size_t>(nreq) * 16);
+            fill(in.data(), in.size(), 5 + t);
+            std::vector<const unsigned char *> ip(static_cast<size_t>(nreq) * ni);
+            std::vector<unsigned char *> op(nreq);
+            std::vector<nxec_agent_req> reqs(nreq);
+            for (int r = 0; r < nreq; r++) {
+              for (int j = 0; j < ni; j++) ip[r * ni + j] = in.data() + (static_cast<size_t>(r) * ni + j) * cs;
+              op[r] = out.data() + static_cast<size_t>(r) * cs;
+              reqs[r] = {ni, 1, row, ip.data() + r * ni, op.data() + r, md5.data() + r * 16};
+            }
+            while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < secs) {
+              if (nxec_agent_encode_batch(ctx, reqs.data(), nreq, cs, 0) != NXEC_OK) ok = false;
+              calls++;
+            }
+          });
+        for (auto &th : pool) th.join();
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const double bytes = static_cast<double>(calls) * nreq * (ni + 1) * cs;
+        std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes + MD5)\", \"threads\": %d, "
+                    "\"chunk\": %d, \"calls\": %ld, \"GiB_s\": %.2f, \"ms_per_call\": %.3f, \"ok\": %s}\n",
+                    threads, cs, static_cast<long>(calls), bytes / dt / (1 << 30),
+                    1e3 * dt * threads / static_cast<double>(calls), ok ? "true" : "false");
+        std::fflush(stdout);
       }
-      long calls = 0;
-      const auto t0 = std::chrono::steady_clock::now();
-      bool ok = true;
-      while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < secs) {
-        ok &= nxec_agent_encode_batch(ctx, reqs.data(), nreq, cs, 0) == NXEC_OK;
-        calls++;
-      }
-      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      const double bytes = static_cast<double>(calls) * nreq * (ni + 1) * cs;
-      std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes + MD5)\", \"threads\": 1, "
-                  "\"chunk\": %d, \"calls\": %ld, \"GiB_s\": %.2f, \"ms_per_call\": %.3f, \"ok\": %s}\n",
-                  cs, calls, bytes / dt / (1 << 30), 1e3 * dt / static_cast<double>(calls), ok ? "true" : "false");
       nxec_ctx_destroy(ctx);
     }
   }

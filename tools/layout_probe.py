@@ -47,16 +47,18 @@ for n, k, cs_kib in geoms:
     cs = cs_kib << 10
     p = n - k
     pats = ["encode", list(range(p)), list(range(k, n)), [1, 4, n - 3, n - 1][:p]]
-    cpads = [0, 4096, 65536] if cs >= (1 << 20) else [0, 4096]
+    cpads = [int(x) for x in os.environ.get("PROBE_CPADS", "0,4096,65536").split(",")]
+    spads = [float(x) for x in os.environ.get("PROBE_SPADS", "0,1").split(",")]  # in chunk strides
+    sgs = os.environ.get("PROBE_SG", "1,8").split(",")
     for cpad in cpads:
         cstride = cs + cpad
-        for spad_chunks in (0, 1):
-            sstride = n * cstride + spad_chunks * cstride
-            for sg in (["1", "8"] if cs >= (2 << 20) else ["1"]):
+        for spad_chunks in spads:
+            sstride = n * cstride + int(spad_chunks * cstride) // 4096 * 4096
+            for sg in (sgs if cs >= (2 << 20) else ["1"]):
                 os.environ["NXEC_STRIPE_GROUP"] = sg
                 res = [rate(n, k, cs, cstride, sstride, op) for op in pats]
                 fr = [f for _, f in res]
-                print(f"({n},{k}) cs {cs_kib:5d} KiB chunk_pad {cpad:6d} stripe_pad {spad_chunks} chunk sg {sg}: "
+                print(f"({n},{k}) cs {cs_kib:5d} KiB chunk_pad {cpad:6d} stripe_pad {spad_chunks:g} chunk sg {sg}: "
                       + " ".join(f"{('enc' if op == 'encode' else ','.join(map(str, op))):>12s} {f:.3f}"
                                  for op, f in zip(pats, fr))
                       + f"  mean {sum(fr) / len(fr):.3f} min {min(fr):.3f}", flush=True)
