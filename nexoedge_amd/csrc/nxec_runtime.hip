@@ -225,6 +225,21 @@ struct nxec_ctx {
   std::vector<Slot *> all_slots;
   std::mutex obj_mu;  // guards obj (one object host call at a time uses it)
   ObjStage obj;
+  // agent-service aggregation (nxec_agent_encode_batch): concurrent callers'
+  // requests join one round; one caller at a time leads and runs the round
+  std::mutex agent_mu;
+  std::condition_variable agent_cv;
+  std::deque<struct AgentJob *> agent_pending;
+  bool agent_leader = false;
+};
+
+struct AgentJob {
+  const nxec_agent_req *reqs;
+  int nreqs;
+  int64_t chunk_size, batch_bytes;
+  int rc = NXEC_OK;
+  bool done = false;
+  std::string error;
 };
 
 namespace {
@@ -931,17 +946,12 @@ int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
 
 }  // namespace
 
-int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
-                            int64_t batch_bytes) {
-  if (!ctx || nreqs < 0 || chunk_size < 0 || (nreqs > 0 && !reqs))
-    return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: invalid arguments");
-  for (int i = 0; i < nreqs; i++) {
-    const nxec_agent_req &r = reqs[i];
-    if (r.ninputs < 1 || r.ninputs > NXEC_MAX_K || r.noutputs < 1 || r.noutputs > NXEC_MAX_N || !r.matrix ||
-        !r.inputs || !r.outputs)
-      return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: request %d malformed", i);
-  }
-  if (nreqs == 0 || chunk_size == 0) return NXEC_OK;
+}  // extern "C"
+
+// One round of agent requests (validated): grouped by matrix, staged through
+// two double-buffered pinned slots of up to batch_bytes each.
+static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
+                             int64_t batch_bytes) {
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
   // group requests by (ninputs, noutputs, matrix): one kernel pass per batch of a group
@@ -1013,6 +1023,77 @@ int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nre
   }
   return rc;
 }
+
+// Requests from concurrent callers are aggregated: a caller queues its job;
+// whichever waiting caller finds no round in progress leads the next one,
+// taking every queued job of the same chunk size, and runs them as ONE set of
+// batches (one MD5 launch per batch covers all callers' outputs, so the ~10 ms
+// MD5 chain of a 1 MiB chunk is paid once per round, not once per call).
+// Rounds use larger staging (>= 1 GiB per slot) than a lone call.
+// NXEC_AGENT_AGGREGATE=0 runs every call on its own.
+extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
+                                       int64_t batch_bytes) {
+  if (!ctx || nreqs < 0 || chunk_size < 0 || (nreqs > 0 && !reqs))
+    return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: invalid arguments");
+  for (int i = 0; i < nreqs; i++) {
+    const nxec_agent_req &r = reqs[i];
+    if (r.ninputs < 1 || r.ninputs > NXEC_MAX_K || r.noutputs < 1 || r.noutputs > NXEC_MAX_N || !r.matrix ||
+        !r.inputs || !r.outputs)
+      return set_error(NXEC_ERR_INVALID, "nxec_agent_encode_batch: request %d malformed", i);
+  }
+  if (nreqs == 0 || chunk_size == 0) return NXEC_OK;
+  static const bool aggregate = [] {
+    const char *e = std::getenv("NXEC_AGENT_AGGREGATE");
+    return !(e && e[0] == '0');
+  }();
+  if (!aggregate) return agent_encode_impl(ctx, reqs, nreqs, chunk_size, batch_bytes);
+  AgentJob job;
+  job.reqs = reqs;
+  job.nreqs = nreqs;
+  job.chunk_size = chunk_size;
+  job.batch_bytes = batch_bytes;
+  std::unique_lock<std::mutex> lk(ctx->agent_mu);
+  ctx->agent_pending.push_back(&job);
+  while (!job.done) {
+    if (ctx->agent_leader) {
+      ctx->agent_cv.wait(lk);
+      continue;
+    }
+    ctx->agent_leader = true;
+    std::vector<AgentJob *> round;
+    const int64_t cs0 = ctx->agent_pending.front()->chunk_size;
+    for (auto it = ctx->agent_pending.begin(); it != ctx->agent_pending.end();) {
+      if ((*it)->chunk_size == cs0) {
+        round.push_back(*it);
+        it = ctx->agent_pending.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    lk.unlock();
+    std::vector<nxec_agent_req> merged;
+    int64_t bb = int64_t(1) << 30;
+    for (AgentJob *j : round) {
+      merged.insert(merged.end(), j->reqs, j->reqs + j->nreqs);
+      bb = std::max(bb, j->batch_bytes);
+    }
+    if (round.size() == 1) bb = round[0]->batch_bytes;  // a lone call keeps its own staging bound
+    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
+    const std::string err = rc ? g_last_error : std::string();
+    lk.lock();
+    for (AgentJob *j : round) {
+      j->rc = rc;
+      j->error = err;
+      j->done = true;
+    }
+    ctx->agent_leader = false;
+    ctx->agent_cv.notify_all();
+  }
+  if (job.rc != NXEC_OK) g_last_error = job.error;
+  return job.rc;
+}
+
+extern "C" {
 
 int nxec_rs_encode_host_batch(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_data, unsigned char *h_parity,
                               int64_t len, int64_t nstripes, int64_t batch_stripes) {

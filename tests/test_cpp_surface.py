@@ -154,3 +154,19 @@ def test_isal_compat_header_drop_in(golden, n, k, cs):
     want = [c["parity_sha256"] for c in golden["encode"] if (c["n"], c["k"], c["cs"]) == (n, k, cs)]
     assert want and lines["PARITY"].strip() == want[0]
     assert lines["DECODED"].strip() == sha(fill_bytes(k * cs, case_seed(n, k, cs)))
+
+
+BATCH = os.path.join(ROOT, "build", "stripe_batch_test")
+
+
+def test_stripe_batch_binary_built():
+    assert os.path.exists(BATCH), "run `make` (build/stripe_batch_test)"
+
+
+@pytest.mark.gpu
+def test_stripe_batch_matches_per_stripe_rscode():
+    """StripeBatch (whole-file encode + MD5 / decode, the batched ChunkManager
+    entry) vs the per-stripe RSCode::encode path the reference takes, every
+    chunk of every stripe, plus OpenSSL MD5 and the decoded file."""
+    r = subprocess.run([BATCH], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("PASSED 0 failures"), (r.stdout[-3000:], r.stderr[-2000:])

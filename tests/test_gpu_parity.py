@@ -568,6 +568,53 @@ def test_agent_encode_batch(gpu_ctx, batch_bytes):
                 assert md5[o].tobytes().hex() == hashlib.md5(w[o].tobytes()).hexdigest()
 
 
+def test_agent_encode_batch_concurrent_callers_aggregate(gpu_ctx):
+    """Agent worker threads calling nxec_agent_encode_batch at once on one
+    context: their requests are aggregated into shared rounds (one MD5 launch
+    per batch for all callers).  Every caller gets exactly its own outputs and
+    digests, bit-exact vs the oracle and hashlib; mixed chunk sizes run in
+    separate rounds."""
+    import hashlib
+    import threading
+
+    n, k = 16, 12
+    jobs, errors = [], []
+    for t in range(8):
+        rng = np.random.default_rng(100 + t)
+        cs = 65536 if t % 3 else 70001
+        reqs, want = [], []
+        for r in range(12):
+            if (t + r) % 2:
+                _, _, rm = nxec.rs_plan(n, k, [(t + r) % n], True)
+                m = rm[:, 4:8]
+            else:
+                m = np.ones((1, 3), dtype=np.uint8)
+            ins = [rng.integers(0, 256, size=cs, dtype=np.uint8) for _ in range(m.shape[1])]
+            outs = [np.zeros(cs, dtype=np.uint8) for _ in range(m.shape[0])]
+            md5 = np.zeros((m.shape[0], 16), dtype=np.uint8)
+            reqs.append((m, ins, outs, md5))
+            want.append(oracle.matmul(m, ins))
+        jobs.append((cs, reqs, want))
+
+    def work(j):
+        try:
+            cs, reqs, _ = jobs[j]
+            for _ in range(3):
+                gpu_ctx.agent_encode_batch(reqs, cs)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(j,)) for j in range(len(jobs))]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not errors, errors
+    for cs, reqs, want in jobs:
+        for (m, ins, outs, md5), w in zip(reqs, want):
+            for o in range(m.shape[0]):
+                assert np.array_equal(outs[o], w[o])
+                assert md5[o].tobytes().hex() == hashlib.md5(w[o].tobytes()).hexdigest()
+
+
 @pytest.mark.parametrize("batch", [0, 2])
 def test_encode_object_host_matches_device(gpu_ctx, batch):
     """Host-inclusive object write (H2D -> encode -> MD5 -> D2H, three streams)
