@@ -59,6 +59,10 @@ def parse(argv=None):
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
+    ap.add_argument("--layout", choices=["auto", "natural", "recover"], default="auto",
+                    help="HBM batch layout: natural = packed [stripe][n][cs]; auto = nxec_batch_layout (padded "
+                         "chunk stride for chunks >= 2 MiB); recover = nxec_batch_layout(RECOVER_HEAVY) (odd "
+                         "stripe stride in 1 MiB units)")
     return ap.parse_args(argv)
 
 
@@ -221,21 +225,31 @@ class Workload:
         self.buffers, self.roof_kernel, self.stripes = buffers, roof_kernel, stripes
 
 
+def layout(args, n, cs):
+    """(chunk_stride, stripe_stride, description) of the batch layout --layout selects."""
+    if args.layout == "natural":
+        return cs, n * cs, "packed [stripe][n][cs]"
+    flags = nxec.LAYOUT_RECOVER_HEAVY if args.layout == "recover" else 0
+    c, st = nxec.batch_layout(n, cs, flags)
+    return c, st, f"nxec_batch_layout({args.layout}): chunk stride {c} B, stripe stride {st} B"
+
+
 def wl_rs10_4(args, ctx, stream, rank):
     """Configs 2+3: RS(10,4) encode + 4-erasure recover, 1 MiB chunks, 4096 stripes."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
-    p, e, stripe = n - k, len(PATTERNS[0]), n * cs
+    p, e = n - k, len(PATTERNS[0])
+    cst, stripe, lay = layout(args, n, cs)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xC0FFEE + rank * 7919)  # synthetic data; parity region overwritten by encode
     ops = [
-        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream), ns * (k + p) * cs),
-        ("decode", lambda i: ctx.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], buf.ptr, cs, stripe, cs, ns, stream),
+        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream), ns * (k + p) * cs),
+        ("decode", lambda i: ctx.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], buf.ptr, cst, stripe, cs, ns, stream),
          ns * (k + e) * cs),
     ]
     config = {
         "workload": f"RS(10,4) (n,k)=({n},{k}) encode + {e}-erasure recover, {cs >> 10} KiB chunks, "
                     f"{ns}-stripe batch per GPU, [stripe][chunk][byte] in HBM",
-        "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": PATTERNS,
+        "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": PATTERNS, "layout": lay,
         "byte_accounting": "encode (k+p)*cs + decode (k+e)*cs per stripe (ISA-L erasure_code_perf.c)",
         "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
     }
@@ -280,18 +294,18 @@ def wl_mixed16(args, ctx, stream, rank):
     """Config 5: RS(16,4) alternating encode / 4-erasure decode at one chunk size;
     the stripe count fills ~args.gib GiB per GPU."""
     n, k, cs = 20, 16, args.chunk
-    stripe = n * cs
+    cst, stripe, lay = layout(args, n, cs)
     ns = max(1, int(args.gib * (1 << 30)) // stripe)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xFACE + rank)
     pats = ([0, 1, 2, 3], [16, 17, 18, 19], [1, 4, 17, 19])
     ops = [
-        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream), ns * n * cs),
-        ("decode", lambda i: ctx.rs_recover(n, k, pats[i % 3], buf.ptr, cs, stripe, cs, ns, stream), ns * n * cs),
+        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream), ns * n * cs),
+        ("decode", lambda i: ctx.rs_recover(n, k, pats[i % 3], buf.ptr, cst, stripe, cs, ns, stream), ns * n * cs),
     ]
     config = {"workload": f"RS(16,4) (n,k)=(20,16) encode + 4-erasure recover, {cs >> 10} KiB chunks, {ns} stripes "
                           f"(~{args.gib} GiB) per GPU",
-              "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": pats,
+              "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": pats, "layout": lay,
               "launch": json.loads(ctx.describe_launch(4, k, cs, ns))}
     return Workload("mixed16", f"GiB/s RS(16,4) encode+decode, {cs >> 10} KiB chunks, device-resident", config, ops,
                     [buf], "k_mul_vec<K=16,R=8> (encode launch)", ns)

@@ -164,6 +164,21 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
                            unsigned char *d_out, int64_t out_chunk_stride, int64_t out_stripe_stride, int64_t len,
                            int64_t nstripes, void *stream);
 
+/* The library's recommended HBM layout of a [stripe][chunk] batch with chunks
+ * of `len` bytes (chunk c of stripe s at base + s*stripe_stride +
+ * c*chunk_stride).  The batch layout is the caller's choice (every entry point
+ * takes both strides); these strides avoid the DRAM channel/bank aliasing that
+ * power-of-two chunk strides cause (profiles/r02_layout_*.log):
+ *  - chunks >= 2 MiB: chunk_stride = len + 2 KiB (RS(16,4) 4 MiB: 0.71 -> 0.76
+ *    of 8 TB/s, every erasure pattern >= 0.75);
+ *  - NXEC_LAYOUT_RECOVER_HEAVY with an even number of 1 MiB-multiple chunks:
+ *    stripe_stride padded by one chunk to an odd multiple (RS(10,4) 1 MiB
+ *    scattered 4-erasure recover 0.71 -> 0.78, encode 0.80 -> 0.79);
+ *  - otherwise the packed layout (chunk_stride = len rounded up to 16,
+ *    stripe_stride = n * chunk_stride). */
+#define NXEC_LAYOUT_RECOVER_HEAVY 1
+int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride);
+
 /* Host-resident batch encode (the proxy write path): h_data [s][k][len] in,
  * h_parity [s][n-k][len] out, both host memory.  When both are pinned or
  * registered (device-mapped) the kernel reads and writes them over PCIe

@@ -104,6 +104,7 @@ _PROTOS = {
     "nxec_checksum": (C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint64), vp]),
     "nxec_describe_launch": (C.c_int, [vp, C.c_int, C.c_int, i64, i64, C.c_char_p, C.c_int]),
     "nxec_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(vp)]),
+    "nxec_batch_layout": (C.c_int, [C.c_int, i64, C.c_int, C.POINTER(i64), C.POINTER(i64)]),
     "nxec_host_free": (C.c_int, [vp]),
     "nxec_host_arena_owns": (C.c_int, [vp]),
     "nxec_host_arena_stats": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),

@@ -995,11 +995,14 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
       MulArgs b = a;
       b.queue_slot = static_order() ? -1 : static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
       b.tiles_per_grab = tiles_per_grab(b);
-      // chunks of >= 2 MiB: walk groups of 8 stripes column-major, so the
-      // in-flight window spans 8 stripes like it does at 1 MiB (4 MiB chunk
-      // stride: 0.655 -> 0.711 of 8 TB/s; 2 MiB neutral; 1 MiB and below stay
-      // stripe-major, profiles/r01_chunk_stride_group.log)
-      b.stripe_group = (b.vec_count + kBlock - 1) / kBlock >= 128 ? 8 : 1;
+      // chunks of >= 2 MiB at a power-of-two-aligned chunk stride: walk groups
+      // of 8 stripes column-major, so the in-flight window spans 8 stripes
+      // like it does at 1 MiB (4 MiB stride: 0.655 -> 0.711 of 8 TB/s,
+      // profiles/r01_chunk_stride_group.log).  A padded stride (the
+      // recommended layout, nxec_batch_layout) runs best stripe-major
+      // (4 MiB + 2 KiB: 0.758 at sg 1, profiles/r02_layout_sweep.log).
+      const bool aliased = a.src_ptrs != nullptr || a.src_chunk_stride % (int64_t(1) << 20) == 0;
+      b.stripe_group = ((b.vec_count + kBlock - 1) / kBlock >= 128 && aliased) ? 8 : 1;
       if (const char *e = std::getenv("NXEC_STRIPE_GROUP")) b.stripe_group = static_cast<uint32_t>(std::max(1, std::atoi(e)));
       b.vec_begin = a.vec_begin + parts[pi][0];
       b.vec_count = parts[pi][1];

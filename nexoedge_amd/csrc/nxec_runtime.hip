@@ -645,6 +645,19 @@ int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t
   return launch_md5(&r, 1, pick_stream(ctx, stream), d_ok, d_nbad);
 }
 
+int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride) {
+  if (n < 1 || n > NXEC_MAX_N || len < 0 || !chunk_stride || !stripe_stride)
+    return set_error(NXEC_ERR_INVALID, "nxec_batch_layout: invalid arguments");
+  constexpr int64_t kMiB = int64_t(1) << 20;
+  int64_t cs = (len + 15) / 16 * 16;
+  if (len >= 2 * kMiB) cs += 2048;  // break the power-of-two chunk stride (profiles/r02_layout_sweep.log)
+  int64_t ss = cs * n;
+  if ((flags & NXEC_LAYOUT_RECOVER_HEAVY) && cs % kMiB == 0 && (ss / kMiB) % 2 == 0) ss += cs;
+  *chunk_stride = cs;
+  *stripe_stride = ss;
+  return NXEC_OK;
+}
+
 int nxec_object_layout(int n, int k, int64_t length, int64_t max_chunk_size, int64_t *nstripes,
                        int64_t *full_stripes, int64_t *last_chunk_size) {
   if (!valid_nk(n, k) || length < 0 || max_chunk_size <= 0 || !nstripes || !full_stripes || !last_chunk_size)

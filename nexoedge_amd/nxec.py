@@ -79,6 +79,16 @@ def decode_matrix(n: int, k: int, input_ids: Sequence[int], targets: Sequence[in
     return out[: len(targets)]
 
 
+LAYOUT_RECOVER_HEAVY = 1
+
+
+def batch_layout(n: int, length: int, flags: int = 0):
+    """(chunk_stride, stripe_stride) of the library's recommended batch layout (nxec_batch_layout)."""
+    c, st = C.c_int64(), C.c_int64()
+    check(lib.nxec_batch_layout(n, length, flags, C.byref(c), C.byref(st)), "nxec_batch_layout")
+    return c.value, st.value
+
+
 def _groups(groups: Sequence[Sequence[int]]):
     offs = [0]
     flat = []
