@@ -54,7 +54,6 @@ def parse(argv=None):
     ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true", default=True,
                     help="also time the pinned H2D->encode->D2H pipeline (default on; N=1 headline workload only)")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
     ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files", "config1"]), default="rs10_4",
                     help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
@@ -202,19 +201,34 @@ def cpu_baseline(args, n, k, cs):
     return out
 
 
-def load_traffic(path, launch_bytes):
-    """HBM bytes per launch from the committed PMC summary (profiles/rNN_pmc_traffic.json,
-    measured on the 4096-stripe headline launch); for another batch size the
-    measured traffic/algorithmic ratio is applied to this launch's bytes."""
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        hbm, alg = d.get("hbm_bytes_per_launch"), d.get("algorithmic_bytes_per_launch")
-        if hbm is None or not alg:
-            return None
-        return hbm if alg == launch_bytes else int(round(hbm / alg * launch_bytes))
-    except (OSError, ValueError):
+PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
+    ("rs10_4", 1 << 20, "auto"): ("r02_pmc_rs10_4.json", "encode"),
+    ("rs10_4", 1 << 20, "natural"): ("r02_pmc_rs10_4.json", "encode"),
+    ("rs10_4", 1 << 20, "recover"): ("r02_pmc_rs10_4_layout_recover.json", "encode"),
+    ("mixed16", 4 << 20, "auto"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
+    ("mixed16", 4 << 20, "recover"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
+    ("mixed16", 4 << 20, "natural"): ("r02_pmc_mixed16_4m_packed.json", "encode"),
+    ("repair12", 1 << 20, "auto"): ("r02_pmc_repair12.json", "repair_fused_perm12"),
+}
+
+
+def load_traffic(args, wl_name, launch_bytes):
+    """HBM bytes per launch of the roofline kernel from the committed PMC passes
+    (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 x2 read correction): the
+    measured traffic/algorithmic ratio of that op's dispatches times this
+    launch's algorithmic bytes.  None when no pass covers this workload."""
+    key = PMC_SUMMARIES.get((wl_name, args.chunk, args.layout))
+    if key is None:
         return None
+    try:
+        with open(os.path.join(ROOT, "profiles", key[0])) as f:
+            disp = [d for d in json.load(f)["dispatches"] if d["op"] == key[1]]
+    except (OSError, ValueError, KeyError):
+        return None
+    if not disp:
+        return None
+    ratio = sum(d["hbm_bytes"] / d["algorithmic_bytes"] for d in disp) / len(disp)
+    return int(round(ratio * launch_bytes))
 
 
 class Workload:
@@ -631,7 +645,7 @@ def main():
         # roofline of the dominant kernel: algorithmic bytes per launch / event-timed launch duration
         b0 = wl.ops[0][2]
         gbs0 = b0 / (op_ms[0] * 1e-3) / 1e9
-        traffic = load_traffic(args.pmc_summary, b0) if wl.name == "rs10_4" else None
+        traffic = load_traffic(args, wl.name, b0)
         result = {
             "metric": wl.metric,
             "value": round(total_bytes / elapsed / GIB, 2),

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -272,10 +273,23 @@ bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
   Slot *s = nullptr;
   {
+    // best fit: the smallest free slot that holds `bytes`, else the largest
+    // (grown below) -- so callers of different sizes do not keep re-pinning
+    // each other's slots (hipHostMalloc of a GiB costs ~0.1 s)
     std::lock_guard<std::mutex> lk(ctx->slot_mu);
-    if (!ctx->free_slots.empty()) {
-      s = ctx->free_slots.back();
-      ctx->free_slots.pop_back();
+    int best = -1;
+    for (int i = 0; i < static_cast<int>(ctx->free_slots.size()); i++) {
+      const size_t c = ctx->free_slots[i]->cap;
+      if (best < 0) {
+        best = i;
+        continue;
+      }
+      const size_t b = ctx->free_slots[best]->cap;
+      if ((c >= bytes && (b < bytes || c < b)) || (c < bytes && b < bytes && c > b)) best = i;
+    }
+    if (best >= 0) {
+      s = ctx->free_slots[best];
+      ctx->free_slots.erase(ctx->free_slots.begin() + best);
     }
   }
   if (!s) {
@@ -961,10 +975,19 @@ int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
 
 }  // extern "C"
 
+static bool agent_trace() {
+  static const bool t = std::getenv("NXEC_AGENT_TRACE") != nullptr;
+  return t;
+}
+
 // One round of agent requests (validated): grouped by matrix, staged through
 // two double-buffered pinned slots of up to batch_bytes each.
+// on_queued (optional) runs once every batch's copies and kernels are queued,
+// before the call waits for the last two batches: the aggregator hands the
+// next round to another caller there, so its gather and H2D overlap this
+// round's tail (last MD5 chains, D2H, output scatter).
 static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
-                             int64_t batch_bytes) {
+                             int64_t batch_bytes, const std::function<void()> &on_queued = nullptr) {
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
   // group requests by (ninputs, noutputs, matrix): one kernel pass per batch of a group
@@ -991,7 +1014,9 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
       const int64_t nb = std::min<int64_t>(B, int64_t(ids.size() - first));
       AgentBatch &b = slots[cur], &other = slots[cur ^ 1];
       cur ^= 1;
+      const auto tr0 = std::chrono::steady_clock::now();
       if ((rc = agent_finish(reqs, chunk_size, b))) break;  // this slot's previous batch
+      const auto tr1 = std::chrono::steady_clock::now();
       if (!b.slot && (rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
       if (b.slot->cap < size_t(B * per)) {  // grown group: re-acquire a larger slot
         release_slot(ctx, b.slot);
@@ -1008,6 +1033,13 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
         std::memcpy(b.slot->h + (i * ni + j) * stride, reqs[ids[first + i]].inputs[j], chunk_size);
       });
       for (int64_t i = 0; i < nb; i++) b.reqs.push_back(ids[first + i]);
+      if (agent_trace()) {
+        const auto tr2 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "agent batch of %lld: finish-previous %.2f ms, gather %.2f ms (%.1f GB/s)\n",
+                     static_cast<long long>(nb), std::chrono::duration<double, std::milli>(tr1 - tr0).count(),
+                     std::chrono::duration<double, std::milli>(tr2 - tr1).count(),
+                     double(nb) * ni * chunk_size / std::chrono::duration<double>(tr2 - tr1).count() / 1e9);
+      }
       hipStream_t st = b.slot->stream;
       uint8_t *d_in = b.slot->d, *d_out = b.slot->d + b.out_off, *d_md5 = b.slot->d + b.md5_off;
       bool any_md5 = false;
@@ -1026,6 +1058,8 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     }
     if (rc) break;
   }
+  if (!rc) rc = agent_d2h(slots[cur ^ 1]);  // the last batch's D2H: now everything is queued
+  if (on_queued) on_queued();
   for (AgentBatch &b : slots) {
     if (b.slot) {
       int rc2 = rc ? NXEC_OK : agent_finish(reqs, chunk_size, b);
@@ -1091,7 +1125,14 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       bb = std::max(bb, j->batch_bytes);
     }
     if (round.size() == 1) bb = round[0]->batch_bytes;  // a lone call keeps its own staging bound
-    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
+    bool handed_over = false;
+    auto hand_over = [&] {  // the next round may start while this one drains
+      std::lock_guard<std::mutex> g(ctx->agent_mu);
+      ctx->agent_leader = false;
+      handed_over = true;
+      ctx->agent_cv.notify_all();
+    };
+    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb, hand_over);
     const std::string err = rc ? g_last_error : std::string();
     lk.lock();
     for (AgentJob *j : round) {
@@ -1099,7 +1140,7 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       j->error = err;
       j->done = true;
     }
-    ctx->agent_leader = false;
+    if (!handed_over) ctx->agent_leader = false;
     ctx->agent_cv.notify_all();
   }
   if (job.rc != NXEC_OK) g_last_error = job.error;

@@ -36,7 +36,10 @@ int main(int argc, char **argv) {
   CodingOptions opt(n, k, false);
   Coding *code = CodingGenerator::genCoding(CodingScheme::RS, opt);
   if (!code) return 1;
+  // argv[3] = "agent": only the agent-service leg
+  const bool agent_only = argc > 3 && std::strcmp(argv[3], "agent") == 0;
   for (int threads : {1, 4, 16}) {
+    if (agent_only) break;
     for (int op = 0; op < 3; op++) {  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode
       std::atomic<long> stripes{0};
       std::atomic<bool> ok{true};
