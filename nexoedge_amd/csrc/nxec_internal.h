@@ -77,6 +77,9 @@ int debug_poison_next_queue_slot(uint32_t next_tile);
 // Raises the dynamic-LDS limit of every kernel instantiation (once per device).
 int prepare_kernels();
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream);
+// 16-byte-aligned copy by a kernel (dst may be device-mapped pinned host memory:
+// a D2H that does not queue behind SDMA copies)
+int launch_copy16(void *dst, const void *src, size_t bytes, int num_cus, void *stream);
 // One MD5 launch hashes up to kMaxMd5Regions chunk sets: region r covers
 // chunks (s, i), s < nstripes, i < nchunks, at base + s*stripe_stride +
 // i*chunk_stride, each `len` bytes; digest at digests + s*dig_stripe_stride +

@@ -753,6 +753,15 @@ __global__ __launch_bounds__(256) void k_pad_chunks(const PadChunks *__restrict_
   }
 }
 
+// 16-byte vector copy; `dst` may be device-mapped pinned host memory, so a
+// device -> host transfer runs as shader stores over PCIe on the compute
+// queue instead of an SDMA copy (which would queue behind the H2D copies).
+__global__ __launch_bounds__(256) void k_copy16(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 __global__ void k_fill(uint8_t *p, int64_t bytes, uint64_t seed) {
   const int64_t words = (bytes + 7) / 8;
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 7) == 0;
@@ -1130,6 +1139,18 @@ int launch_pad_copy(const PadCopy *d_items, int64_t nitems, void *stream) {
                      static_cast<hipStream_t>(stream), d_items);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_pad_copy");
+}
+
+int launch_copy16(void *dst, const void *src, size_t bytes, int num_cus, void *stream) {
+  if (bytes == 0) return NXEC_OK;
+  if (bytes % 16 || (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
+    return set_error(NXEC_ERR_INVALID, "copy16: unaligned");
+  const int64_t n = static_cast<int64_t>(bytes / 16);
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, static_cast<int64_t>(num_cus) * 4);
+  hipLaunchKernelGGL(k_copy16, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<u32x4 *>(dst), static_cast<const u32x4 *>(src), n);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : hip_fail(e, "launch k_copy16");
 }
 
 int launch_fill(void *d, size_t bytes, uint64_t seed, void *stream) {

@@ -945,18 +945,26 @@ struct AgentBatch {
 // D2H queued first (it waits for the batch's MD5, ~10 ms) blocked the next
 // batch's H2D on the other stream behind it, so batches ran one after the
 // other (tools/agent_probe.py timeline, profiles/r01_agent_timeline.txt).
-int agent_d2h(AgentBatch &b) {
+// The outputs go back by a copy kernel writing the slot's device-mapped pinned
+// staging over PCIe: SDMA copies run one after another on this box, so an
+// SDMA D2H queued between two batches' H2Ds stalled the next H2D by its whole
+// duration (rocprofv3 memory-copy trace, profiles/r02_agent_timeline.txt);
+// the kernel's stores use the link's other direction while the H2Ds stream.
+int agent_d2h(nxec_ctx_t *ctx, AgentBatch &b) {
   if (!b.d2h_bytes) return NXEC_OK;
   const size_t nb = b.d2h_bytes;
   b.d2h_bytes = 0;
+  uint8_t *hv = static_cast<uint8_t *>(host_device_view(b.slot->h));
+  if (hv && nb % 16 == 0 && b.out_off % 16 == 0)
+    return launch_copy16(hv + b.out_off, b.slot->d + b.out_off, nb, ctx->num_cus, b.slot->stream);
   return hip_check(hipMemcpyAsync(b.slot->h + b.out_off, b.slot->d + b.out_off, nb, hipMemcpyDeviceToHost,
                                   b.slot->stream),
                    "agent D2H");
 }
 
-int agent_finish(const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
+int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentBatch &b) {
   if (b.reqs.empty()) return NXEC_OK;
-  if (int rc = agent_d2h(b)) return rc;
+  if (int rc = agent_d2h(ctx, b)) return rc;
   NXEC_HIP(hipStreamSynchronize(b.slot->stream));
   const nxec_agent_req &r0 = reqs[b.reqs[0]];
   const int no = r0.noutputs;
@@ -982,12 +990,8 @@ static bool agent_trace() {
 
 // One round of agent requests (validated): grouped by matrix, staged through
 // two double-buffered pinned slots of up to batch_bytes each.
-// on_queued (optional) runs once every batch's copies and kernels are queued,
-// before the call waits for the last two batches: the aggregator hands the
-// next round to another caller there, so its gather and H2D overlap this
-// round's tail (last MD5 chains, D2H, output scatter).
 static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
-                             int64_t batch_bytes, const std::function<void()> &on_queued = nullptr) {
+                             int64_t batch_bytes) {
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
   // group requests by (ninputs, noutputs, matrix): one kernel pass per batch of a group
@@ -1001,7 +1005,11 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
   }
   const int64_t stride = (chunk_size + 15) / 16 * 16;
   if (batch_bytes <= 0) batch_bytes = int64_t(256) << 20;
-  AgentBatch slots[2];
+  // three staging slots in rotation: batch b gathers into its slot while
+  // batch b-1's H2D runs and batch b-2's MD5 chains finish, so the link never
+  // waits for a gather (two slots left ~6 ms gaps per batch)
+  constexpr int kAgentSlots = 3;
+  AgentBatch slots[kAgentSlots];
   int cur = 0;
   rc = NXEC_OK;
   for (auto &kv : groups) {
@@ -1012,10 +1020,10 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));
     for (size_t first = 0; first < ids.size() && rc == NXEC_OK; first += B) {
       const int64_t nb = std::min<int64_t>(B, int64_t(ids.size() - first));
-      AgentBatch &b = slots[cur], &other = slots[cur ^ 1];
-      cur ^= 1;
+      AgentBatch &b = slots[cur], &other = slots[(cur + kAgentSlots - 1) % kAgentSlots];
+      cur = (cur + 1) % kAgentSlots;
       const auto tr0 = std::chrono::steady_clock::now();
-      if ((rc = agent_finish(reqs, chunk_size, b))) break;  // this slot's previous batch
+      if ((rc = agent_finish(ctx, reqs, chunk_size, b))) break;  // this slot's previous batch
       const auto tr1 = std::chrono::steady_clock::now();
       if (!b.slot && (rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
       if (b.slot->cap < size_t(B * per)) {  // grown group: re-acquire a larger slot
@@ -1054,15 +1062,15 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
         if ((rc = launch_md5(&reg, 1, st))) break;
       }
       b.d2h_bytes = size_t(nb) * (no * stride + (any_md5 ? no * 16 : 0));
-      if ((rc = agent_d2h(other))) break;  // the previous batch's D2H, behind this batch's H2D
+      if ((rc = agent_d2h(ctx, other))) break;  // the previous batch's D2H, behind this batch's H2D
     }
     if (rc) break;
   }
-  if (!rc) rc = agent_d2h(slots[cur ^ 1]);  // the last batch's D2H: now everything is queued
-  if (on_queued) on_queued();
-  for (AgentBatch &b : slots) {
+  if (!rc) rc = agent_d2h(ctx, slots[(cur + kAgentSlots - 1) % kAgentSlots]);  // the last batch's D2H
+  for (int i = 0; i < kAgentSlots; i++) {  // oldest batch first
+    AgentBatch &b = slots[(cur + i) % kAgentSlots];
     if (b.slot) {
-      int rc2 = rc ? NXEC_OK : agent_finish(reqs, chunk_size, b);
+      int rc2 = rc ? NXEC_OK : agent_finish(ctx, reqs, chunk_size, b);
       if (rc) (void)hipStreamSynchronize(b.slot->stream);
       if (!rc) rc = rc2;
       release_slot(ctx, b.slot);
@@ -1125,14 +1133,7 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       bb = std::max(bb, j->batch_bytes);
     }
     if (round.size() == 1) bb = round[0]->batch_bytes;  // a lone call keeps its own staging bound
-    bool handed_over = false;
-    auto hand_over = [&] {  // the next round may start while this one drains
-      std::lock_guard<std::mutex> g(ctx->agent_mu);
-      ctx->agent_leader = false;
-      handed_over = true;
-      ctx->agent_cv.notify_all();
-    };
-    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb, hand_over);
+    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
     const std::string err = rc ? g_last_error : std::string();
     lk.lock();
     for (AgentJob *j : round) {
@@ -1140,7 +1141,7 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       j->error = err;
       j->done = true;
     }
-    if (!handed_over) ctx->agent_leader = false;
+    ctx->agent_leader = false;
     ctx->agent_cv.notify_all();
   }
   if (job.rc != NXEC_OK) g_last_error = job.error;
