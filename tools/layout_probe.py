@@ -47,6 +47,8 @@ for n, k, cs_kib in geoms:
     cs = cs_kib << 10
     p = n - k
     pats = ["encode", list(range(p)), list(range(k, n)), [1, 4, n - 3, n - 1][:p]]
+    if os.environ.get("PROBE_PATS"):  # e.g. "enc;0;15"
+        pats = ["encode" if x == "enc" else [int(c) for c in x.split(",")] for x in os.environ["PROBE_PATS"].split(";")]
     cpads = [int(x) for x in os.environ.get("PROBE_CPADS", "0,4096,65536").split(",")]
     spads = [float(x) for x in os.environ.get("PROBE_SPADS", "0,1").split(",")]  # in chunk strides
     sgs = os.environ.get("PROBE_SG", "1,8").split(",")
