@@ -208,7 +208,9 @@ PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file
     ("mixed16", 4 << 20, "auto"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
     ("mixed16", 4 << 20, "recover"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
     ("mixed16", 4 << 20, "natural"): ("r02_pmc_mixed16_4m_packed.json", "encode"),
-    ("repair12", 1 << 20, "auto"): ("r02_pmc_repair12.json", "repair_fused_perm12"),
+    ("repair12", 1 << 20, "natural"): ("r02_pmc_repair12.json", "repair_fused_perm12"),
+    ("repair12", 1 << 20, "auto"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
+    ("repair12", 1 << 20, "recover"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
 }
 
 
@@ -277,26 +279,26 @@ def wl_repair12(args, ctx, stream, rank):
     unfused agent partial-encode path (racks of 4 chunks: partial 1 x g encodes,
     container_manager.cc:251, then the CAR XOR finalize, rs.cc:94-109)."""
     n, k, cs, ns, g = 16, 12, args.chunk, args.stripes, 4
-    stripe = n * cs
+    cst, stripe, lay = layout(args, n, cs)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xBEEF + rank)
-    ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream)
+    ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream)
     failed = args.failed if args.failed is not None else 0
     racks = [list(range(r, min(r + g, n))) for r in range(0, n, g)]  # chunk i on agent i // g
     G = len(nxec.car_plan(n, k, failed, racks))
     part = nxec.DeviceBuffer(ns * G * cs)
 
     def unfused(i):
-        ctx.rs_car_repair(n, k, failed, racks, buf.ptr, cs, stripe, part.ptr, cs, G * cs, cs, ns, stream)
+        ctx.rs_car_repair(n, k, failed, racks, buf.ptr, cst, stripe, part.ptr, cs, G * cs, cs, ns, stream)
 
     ops = [
-        ("repair_fused", lambda i: ctx.rs_recover(n, k, [failed], buf.ptr, cs, stripe, cs, ns, stream),
+        ("repair_fused", lambda i: ctx.rs_recover(n, k, [failed], buf.ptr, cst, stripe, cs, ns, stream),
          ns * (k + 1) * cs),
         ("repair_car_unfused", unfused, ns * (k + 1 + 2 * G) * cs),
     ]
     config = {"workload": f"RS(12,4) (n,k)=(16,12) single-failure repair of chunk {failed}, racks of {g} chunks "
                           f"({G} partials), {cs >> 10} KiB chunks, {ns} stripes per GPU",
-              "stripes_per_gpu": ns, "chunk_bytes": cs,
+              "stripes_per_gpu": ns, "chunk_bytes": cs, "layout": lay,
               "byte_accounting": "fused (k+1)*cs; CAR unfused (k+1+2G)*cs per stripe (SURVEY 8d)",
               "launch": json.loads(ctx.describe_launch(1, k, cs, ns))}
     kern = config["launch"]["kernel"]

@@ -171,9 +171,12 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * power-of-two chunk strides cause (profiles/r02_layout_*.log):
  *  - chunks >= 2 MiB: chunk_stride = len + 2 KiB (RS(16,4) 4 MiB: 0.71 -> 0.76
  *    of 8 TB/s, every erasure pattern >= 0.75);
- *  - NXEC_LAYOUT_RECOVER_HEAVY with an even number of 1 MiB-multiple chunks:
- *    stripe_stride padded by one chunk to an odd multiple (RS(10,4) 1 MiB
- *    scattered 4-erasure recover 0.71 -> 0.78, encode 0.80 -> 0.79);
+ *  - stripes of 1 MiB-multiple chunks whose size is a power-of-two number of
+ *    MiB: stripe_stride padded by one chunk to an odd multiple (RS(12,4) 1
+ *    MiB: encode 0.80 -> 0.81, single-failure repair 0.74 -> 0.79);
+ *  - NXEC_LAYOUT_RECOVER_HEAVY with any even number of such chunks: the same
+ *    padding (RS(10,4) 1 MiB scattered 4-erasure recover 0.71 -> 0.78, encode
+ *    0.80 -> 0.79);
  *  - otherwise the packed layout (chunk_stride = len rounded up to 16,
  *    stripe_stride = n * chunk_stride). */
 #define NXEC_LAYOUT_RECOVER_HEAVY 1

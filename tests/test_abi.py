@@ -94,3 +94,24 @@ def test_arena_without_device_falls_back():
     rc = _lib.lib.nxec_host_alloc(1 << 20, ctypes.byref(p))
     assert rc in (_lib.NXEC_ERR_NODEV, _lib.NXEC_ERR_NOMEM) and not p.value
     assert _lib.lib.nxec_host_arena_owns(None) == 0
+
+
+def test_batch_layout_policy():
+    """nxec_batch_layout (host-only arithmetic): chunk strides of >= 2 MiB
+    chunks padded by 2 KiB; stripes of a power-of-two number of MiB padded by
+    one chunk; any even number of MiB only when recover-heavy; 256 KiB and
+    64 KiB chunks left packed (profiles/r02_layout_sweep.log)."""
+    M = 1 << 20
+    assert nxec.batch_layout(14, M) == (M, 14 * M)
+    assert nxec.batch_layout(14, M, 1) == (M, 15 * M)
+    assert nxec.batch_layout(16, M) == (M, 17 * M)
+    assert nxec.batch_layout(20, M) == (M, 20 * M)
+    assert nxec.batch_layout(20, M, 1) == (M, 21 * M)
+    assert nxec.batch_layout(20, 256 << 10) == (256 << 10, 20 * (256 << 10))
+    assert nxec.batch_layout(15, M, 1) == (M, 15 * M)  # already odd
+    cs, ss = nxec.batch_layout(20, 4 * M)
+    assert cs == 4 * M + 2048 and ss == 20 * cs
+    for n, ln in [(14, M), (16, M), (20, 4 * M), (6, 3 * M + 5), (4, 2 * M)]:
+        for fl in (0, 1):
+            cs, ss = nxec.batch_layout(n, ln, fl)
+            assert cs >= ln and ss >= n * cs and cs % 16 == 0 and ss % 16 == 0
