@@ -1,0 +1,312 @@
+// Fused RS encode + per-chunk MD5 of a stripe batch on gfx950.
+//
+// The proxy's write path codes every stripe and then hashes every chunk it
+// sends (chunk_manager.cc:66-452: RSCode::encode, then Chunk::computeMD5 at
+// :175 for each of the n chunks).  Run as two kernels, the encode reads the
+// data once (k*cs per stripe) and writes the parity, then the MD5 reads all n
+// chunks again: 2x the HBM traffic of the encode alone, and the parity chains
+// cannot start before the parity exists (encode 9.4 ms + MD5 ~12 ms for 4096
+// RS(10,4) 1 MiB stripes).  Here both run in one kernel over one read:
+//
+//  * A workgroup owns S whole stripes (S*n <= 256 chunks) and walks them
+//    column by column, 256 bytes of every chunk per step.  MD5 is a serial
+//    chain per chunk, so a chunk's bytes must reach its hash lane in order;
+//    every chain of the batch runs at once (one lane each).
+//  * Waves 0-3 ("code"): lane (stripe, 16-byte column vector) loads the k
+//    source vectors of its column for the NEXT step (register ping-pong),
+//    computes the parity of this step through the packed-row LDS product
+//    tables (nxec_device.h), stores the parity to HBM, and drops the k data
+//    vectors and the parity vectors into this step's LDS buffer.
+//  * Waves 4-7 ("hash"): lane h owns chunk h = stripe*n + c; after the step's
+//    barrier it reads its 256-byte row of the buffer (16 ds_read_b128, rows
+//    272 bytes apart so a quarter-wave's rows hit distinct banks) and runs 4
+//    MD5 blocks.  The code waves fill the other buffer meanwhile (two
+//    buffers, one LDS-only barrier per step; global loads and stores stay in
+//    flight across it).
+//  * Every SIMD holds one code and one hash wave.  A wave alone issues one
+//    VALU op per 4 cycles and a SIMD can issue one per 2 (MI355X_MICROARCH.md
+//    'Wave scheduling'), so the chains run at their single-wave rate while the
+//    code wave's lookups use the other half of the issue slots and the LDS.
+//    The chain (16 384 blocks x ~324 VALU x 4 cycles per 1 MiB chunk) is the
+//    floor of the whole write: ~9-10 ms instead of the two kernels' 21 ms.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdlib>
+#include <utility>
+
+#include "nxec_device.h"
+#include "nxec_internal.h"
+
+namespace nxec {
+
+namespace {
+
+using dev::build_tables;
+using dev::ld_stream;
+using dev::lookup16;
+using dev::md5_block;
+using dev::md5_init;
+using dev::md5_pad_aligned;
+using dev::rows_of;
+using dev::st_stream;
+using dev::u32x4;
+
+constexpr int kEmBlock = 512;                  // 4 code waves + 4 hash waves
+constexpr int kEmCodeLanes = 256;
+constexpr int kEmVecs = kEncMd5Step / 16;      // 16-byte column vectors per chunk per step
+constexpr int kEmRow = kEncMd5Step + 16;       // LDS row stride: bank rotation for the hash lanes' reads
+constexpr int kEmMaxRows = 256;                // chunks per workgroup = hash lanes
+constexpr int kEmMaxStripes = kEmCodeLanes / kEmVecs;
+constexpr int kEmLds = 160 * 1024;
+constexpr int kEmBufMax = 2 * kEmMaxRows * kEmRow;
+
+// table replication: 2 copies where they fit beside two full buffers
+template <int K>
+constexpr int em_r() {
+  return kEmBufMax + K * 1024 * 2 <= kEmLds ? 2 : 1;
+}
+
+// prefetch ring depth: as many 4K-VGPR source buffers as fit in ~170 VGPRs
+template <int K>
+constexpr int em_depth() {
+  return K * 4 * 4 <= 170 ? 4 : K * 4 * 3 <= 170 ? 3 : 2;
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// PROBE (design probes only, K = 10, NXEC_EM_PROBE; outputs are NOT valid):
+// bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
+// the table lookups (parity = first source), to time each role alone.
+template <int K, int PROBE = 0>
+__global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
+  constexpr int R = em_r<K>();
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int n = K + a.p;
+  const int S = a.stripes_per_group;
+  uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
+  uint8_t *buf = lds + K * 1024 * R;
+  const uint32_t buf_bytes = static_cast<uint32_t>(S * n * kEmRow);
+  build_tables<R>(a.coef, K, a.p, tab);
+  __syncthreads();
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
+  const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
+  const int nsteps = static_cast<int>(a.len / kEncMd5Step);
+
+  if (threadIdx.x < kEmCodeLanes) {
+    // ---- code waves: lane = (stripe ls, column vector v) ----
+    // Lanes past the group's last stripe (a partial last group) shadow lane
+    // (0, v): same loads, same values stored to the same places.  Everything
+    // stays unconditional, so the compiler's vmcnt bookkeeping sees one path
+    // and waits only for the ring slot it consumes.
+    const int item = threadIdx.x;
+    const int ls = item < nS * kEmVecs ? item / kEmVecs : 0, v = item % kEmVecs;
+    const uint8_t *src = a.data + (s0 + ls) * a.data_stripe_stride + v * 16;
+    uint8_t *dst = a.parity + (s0 + ls) * a.parity_stripe_stride + v * 16;
+    uint8_t *row = buf + ls * n * kEmRow + v * 16;
+    const char *tl = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
+    auto load = [&](int step, u32x4(&d)[K]) {
+      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+#pragma unroll
+      for (int j = 0; j < K; j++) d[j] = ld_stream(src + j * a.data_chunk_stride + off);
+    };
+    auto run = [&](int step, const u32x4(&d)[K]) {
+      uint8_t *rb = row + (step & 1) * buf_bytes;
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int j = 0; j < K; j++) {
+        *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+        if (PROBE & 2) {
+          if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
+        } else {
+          lookup16<R>(tl + j * 1024 * R, d[j], acc);
+        }
+        // materialise the accumulators per source: left alone, LLVM turns
+        // the XOR chains into trees over all k sources, which keeps 16
+        // lookup results per source live at once (spills from k = 10)
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
+      }
+      uint32_t o[4][4];
+      rows_of(acc, o);
+      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++) {
+        if (r < a.p) {  // wave-uniform
+          const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
+          st_stream(dst + r * a.parity_chunk_stride + off, pv);
+          *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = pv;
+        }
+      }
+      lds_barrier();  // this step's buffer is full
+    };
+    // ring of D register buffers: the loads of step s + D - 1 go out before
+    // step s is computed, so ~(D-1) steps of sources are in flight per lane
+    // (one step ahead left the chip at ~0.65 of 8 TB/s with no arithmetic at
+    // all).  Loads past the last step re-read it, so they stay unconditional.
+    constexpr int D = em_depth<K>();
+    u32x4 ring[D][K];
+    const int last = nsteps - 1;
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
+    // whole rounds of D steps without exits (an exit inside the unrolled
+    // round merges ring states at the loop head, and the compiler then drains
+    // every load there), then the < D leftover steps
+    int step = 0;
+    for (; step + D <= nsteps; step += D) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) {
+      if (step + j < nsteps) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+    return;
+  }
+
+  // ---- hash waves: lane h = chunk (h / n, h % n) of the group = LDS row h ----
+  if (a.hash_prio) __builtin_amdgcn_s_setprio(1);
+  const int h = threadIdx.x - kEmCodeLanes;
+  const bool active = h < nS * n;
+  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
+  uint32_t st[4];
+  md5_init(st);
+  // The row of step s is read right after barrier s, while the lane hashes
+  // step s - 1 from registers: the reads (queued behind the code waves'
+  // lookups in the LDS) get a whole step to land.  They are complete before
+  // barrier s + 1 (its fence waits for them), so the code waves may refill
+  // that buffer afterwards.
+  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
+    const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
+#pragma unroll
+    for (int i = 0; i < kEmVecs; i++) {
+      const u32x4 x = p[i];
+      m[4 * i] = x.x;
+      m[4 * i + 1] = x.y;
+      m[4 * i + 2] = x.z;
+      m[4 * i + 3] = x.w;
+    }
+  };
+  auto hash = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
+    if (PROBE & 1) {
+#pragma unroll
+      for (int i = 0; i < kEncMd5Step / 4; i++) st[i & 3] ^= m[i];
+    } else {
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+    }
+  };
+  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
+  lds_barrier();
+  if (active) fetch(0, m0);
+  int step = 1;
+  for (; step + 2 <= nsteps; step += 2) {
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+    }
+    lds_barrier();
+    if (active) {
+      fetch(step + 1, m0);
+      hash(m1);
+    }
+  }
+  if (step < nsteps) {  // nsteps even: one step left
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+      hash(m1);
+    }
+  } else if (active) {
+    hash(m0);
+  }
+  if (active) {
+    md5_pad_aligned(st, static_cast<uint64_t>(a.len));
+    const int ls = h / n, c = h - ls * n;
+    uint8_t *out = a.digests + (s0 + ls) * a.digest_stripe_stride + c * 16;
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+  }
+}
+
+using EmKernel = void (*)(const EncMd5Args);
+template <int... Ks>
+constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_encode_md5<Ks + 1>...}};
+}
+const std::array<EmKernel, kEncMd5MaxK> kEm = em_table(std::make_integer_sequence<int, kEncMd5MaxK>{});
+
+const EmKernel kEmProbe[4] = {&k_encode_md5<10, 0>, &k_encode_md5<10, 1>, &k_encode_md5<10, 2>, &k_encode_md5<10, 3>};
+
+int em_r_of(int k) { return 2 * kEmMaxRows * kEmRow + k * 1024 * 2 <= kEmLds ? 2 : 1; }
+
+}  // namespace
+
+bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t data_cs, int64_t data_ss,
+                         const void *parity, int64_t parity_cs, int64_t parity_ss) {
+  if (k < 1 || k > kEncMd5MaxK || p < 1 || p > kMaxRowsPerPass) return false;
+  if (len <= 0 || len % kEncMd5Step != 0 || len / kEncMd5Step >= (int64_t(1) << 31)) return false;
+  if (const char *e = std::getenv("NXEC_FUSED_MD5"))
+    if (e[0] == '0') return false;  // A/B: two kernels (encode, then MD5)
+  const uint64_t bits = reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity) |
+                        static_cast<uint64_t>(data_cs) | static_cast<uint64_t>(data_ss) |
+                        static_cast<uint64_t>(parity_cs) | static_cast<uint64_t>(parity_ss);
+  return (bits & 15) == 0;
+}
+
+int prepare_encode_md5() {
+  for (int k = 1; k <= kEncMd5MaxK; k++) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEm[k - 1]),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_encode_md5): %s", hipGetErrorString(e));
+  }
+  for (EmKernel fn : kEmProbe) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_encode_md5 probe): %s", hipGetErrorString(e));
+  }
+  return NXEC_OK;
+}
+
+int launch_encode_md5(const EncMd5Args &in, int num_cus, void *stream) {
+  if (in.nstripes <= 0) return NXEC_OK;
+  EncMd5Args a = in;
+  const int n = a.k + a.p;
+  // as many stripes per workgroup as its 256 hash lanes and code lanes hold,
+  // but spread over every CU first (each chain is ~9 ms of one lane whatever
+  // the batch: fewer stripes per CU means shorter code steps, not shorter chains)
+  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / n);
+  const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
+  if (per_cu < S) S = per_cu;
+  a.stripes_per_group = static_cast<int32_t>(S);
+  a.hash_prio = 0;
+  if (const char *e = std::getenv("NXEC_EM_PRIO")) a.hash_prio = std::atoi(e);
+  const int64_t grid = (a.nstripes + S - 1) / S;
+  if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
+  const int lds = a.k * 1024 * em_r_of(a.k) + static_cast<int>(2 * S * n * kEmRow);
+  EmKernel fn = kEm[a.k - 1];
+  if (const char *e = std::getenv("NXEC_EM_PROBE"))
+    if (a.k == 10) fn = kEmProbe[std::atoi(e) & 3];
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_encode_md5: %s", hipGetErrorString(e));
+}
+
+}  // namespace nxec

@@ -144,6 +144,33 @@ struct Md5Item {
 };
 int launch_md5_list(const Md5Item *d_items, int64_t nitems, void *stream);
 
+// Fused encode + MD5 of every chunk (nxec_encode_md5.hip): parity row r of
+// stripe s at parity + s*parity_stripe_stride + r*parity_chunk_stride, data
+// chunk j at data + s*data_stripe_stride + j*data_chunk_stride; digest of
+// chunk c (data c < k, parity k + r) at digests + s*digest_stripe_stride + c*16.
+// Chunks are walked in steps of kEncMd5Step bytes (len a multiple of it).
+constexpr int kEncMd5Step = 256;
+constexpr int kEncMd5MaxK = 20;
+struct EncMd5Args {
+  const uint8_t *data;
+  int64_t data_chunk_stride, data_stripe_stride;
+  uint8_t *parity;
+  int64_t parity_chunk_stride, parity_stripe_stride;
+  uint8_t *digests;
+  int64_t digest_stripe_stride;
+  int64_t len, nstripes;
+  int32_t k, p;
+  int32_t stripes_per_group;  // set by launch_encode_md5
+  int32_t hash_prio;          // hash waves at s_setprio 1 (set by launch_encode_md5)
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
+};
+// k <= kEncMd5MaxK, 1 <= p <= 4, len a positive multiple of kEncMd5Step,
+// 16-byte aligned buffers and strides (NXEC_FUSED_MD5=0 disables, for A/B)
+bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t data_cs, int64_t data_ss,
+                         const void *parity, int64_t parity_cs, int64_t parity_ss);
+int prepare_encode_md5();
+int launch_encode_md5(const EncMd5Args &a, int num_cus, void *stream);
+
 }  // namespace nxec
 
 #endif

@@ -35,6 +35,7 @@
 #include <cstring>
 #include <utility>
 
+#include "nxec_device.h"
 #include "nxec_internal.h"
 
 namespace nxec {
@@ -51,44 +52,17 @@ constexpr int kPrefetchMaxKCopy = 8;  // k = 10 with copies fits (123 VGPRs) but
 constexpr int kPermPrefetchMaxK = 4;
 constexpr int kPermMaxK = 13;  // beyond this the single-row VALU kernel would spill (128-VGPR budget)
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 constexpr int kRingBytes = 16;  // work-queue broadcast ring, after the tables in dynamic LDS
 constexpr bool queue_fits(int table_bytes) { return table_bytes + kRingBytes <= kLdsBytes; }
 
-// Streaming (nontemporal) 16-byte accesses: every source byte is read once and
-// every parity byte written once, so keep them from displacing the tables'
-// neighbours in L2/MALL.  Measured +2-3 % at RS(10,4) 1 MiB (tools/microbench/tune_mul.hip).
-__device__ __forceinline__ u32x4 ld_stream(const uint8_t *p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-}
-__device__ __forceinline__ void st_stream(uint8_t *p, u32x4 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-}
+using dev::build_tables;
+using dev::gf_mul_dev;
+using dev::ld_stream;
+using dev::lookup16;
+using dev::rows_of;
+using dev::st_stream;
+using dev::u32x4;
 
-__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    p ^= (b & 1u) ? a : 0u;
-    a = (a << 1) ^ ((a & 0x80u) ? 0x11du : 0u);
-    b >>= 1;
-  }
-  return p;
-}
-
-// entry x of source j: byte r = c(r, j) * x (coef row-major rows x k)
-template <int R>
-__device__ __forceinline__ void build_tables(const uint8_t *coef, int k, int rows, uint32_t *tab) {
-  for (int i = threadIdx.x; i < k * 256; i += blockDim.x) {
-    const int j = i >> 8;
-    const uint32_t x = static_cast<uint32_t>(i & 255);
-    uint32_t e = 0;
-    for (int r = 0; r < rows; r++) e |= gf_mul_dev(coef[r * k + j], x) << (8 * r);
-#pragma unroll
-    for (int c = 0; c < R; c++) tab[i * R + c] = e;
-  }
-}
 template <int R>
 __device__ __forceinline__ void build_tables(const MulArgs &a, int k, uint32_t *tab) {
   build_tables<R>(a.coef, a.k, a.rows, tab);
@@ -113,18 +87,7 @@ __device__ __forceinline__ const uint8_t *src_chunk(const MulArgs &a, uint32_t s
 template <bool GATHER>
 __device__ __forceinline__ void store_rows(const MulArgs &a, uint32_t s, uint32_t v, const uint32_t acc[16]) {
   uint32_t o[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
-    const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);
-    const uint32_t hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
-    const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
-    const uint32_t hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
-    o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
-    o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
-    o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
-    o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
-  }
+  rows_of(acc, o);
 #pragma unroll
   for (int r = 0; r < kMaxRowsPerPass; r++) {
     if (r < a.rows) st_stream(dst_row<GATHER>(a, s, r) + static_cast<size_t>(v) * 16, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
@@ -135,34 +98,10 @@ __device__ __forceinline__ void store_rows(const MulArgs &a, uint32_t s, uint32_
 __device__ __forceinline__ void store_rows_ptr(uint8_t *row0, int64_t row_stride, int rows, uint32_t v,
                                                const uint32_t acc[16]) {
   uint32_t o[4][4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
-    const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u);
-    const uint32_t hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
-    const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u);
-    const uint32_t hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
-    o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
-    o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
-    o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
-    o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
-  }
+  rows_of(acc, o);
 #pragma unroll
   for (int r = 0; r < kMaxRowsPerPass; r++)
     if (r < rows) st_stream(row0 + r * row_stride + static_cast<size_t>(v) * 16, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
-}
-
-template <int R>
-__device__ __forceinline__ void lookup16(const char *tb, const u32x4 d, uint32_t acc[16]) {
-  const uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t x = (w[q] >> (8 * b)) & 0xffu;
-      acc[4 * q + b] ^= *reinterpret_cast<const uint32_t *>(tb + x * (4 * R));
-    }
-  }
 }
 
 // Column vector v (relative to the launch's vec_begin) of stripe s for tile t;
@@ -667,16 +606,7 @@ __global__ __launch_bounds__(256) void k_mul_list(const ListArgs a) {
       for (int i = 0; i < 16; i++) acc[i] = 0;
       for (int j = 0; j < k; j++) lookup16<1>(tl + j * 1024, ld_stream(st.src + j * st.src_cs + off), acc);
       uint32_t o[4][4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const uint32_t a0 = acc[4 * q], a1 = acc[4 * q + 1], a2 = acc[4 * q + 2], a3 = acc[4 * q + 3];
-        const uint32_t lo01 = __builtin_amdgcn_perm(a1, a0, 0x05010400u), hi01 = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
-        const uint32_t lo23 = __builtin_amdgcn_perm(a3, a2, 0x05010400u), hi23 = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
-        o[0][q] = __builtin_amdgcn_perm(lo23, lo01, 0x05040100u);
-        o[1][q] = __builtin_amdgcn_perm(lo23, lo01, 0x07060302u);
-        o[2][q] = __builtin_amdgcn_perm(hi23, hi01, 0x05040100u);
-        o[3][q] = __builtin_amdgcn_perm(hi23, hi01, 0x07060302u);
-      }
+      rows_of(acc, o);
 #pragma unroll
       for (int r = 0; r < kMaxRowsPerPass; r++)
         if (r < a.rows) st_stream(drow0 + r * st.dst_cs, u32x4{o[r][0], o[r][1], o[r][2], o[r][3]});
@@ -936,7 +866,7 @@ int prepare_kernels() {
     hipError_t e = raise(fn, NXEC_MAX_K * 1024);
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(dyn/bytes)");
   }
-  return NXEC_OK;
+  return prepare_encode_md5();
 }
 
 // Work-queue run length: about 12 tiles' worth of chunk traffic per grab (a

@@ -20,60 +20,15 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "nxec_device.h"
 #include "nxec_internal.h"
 
 namespace nxec {
 
 namespace {
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
-
-// Round r (0..63): function, message index and shift per RFC 1321 §3.4;
-// K[r] = floor(|sin(r+1)| * 2^32).
-constexpr uint32_t kMd5K[64] = {
-    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
-    0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
-    0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
-    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
-    0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
-    0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
-    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
-    0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
-
-template <int R>
-__device__ __forceinline__ void md5_round(uint32_t &a, uint32_t b, uint32_t c, uint32_t d, const uint32_t (&m)[16]) {
-  constexpr int kShift[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
-  constexpr int q = R / 16;
-  // one v_bitop3_b32 per round function (truth table over (b, c, d), bit
-  // index 4b+2c+d): F = b ? c : d (0xCA), G = d ? b : c (0xE4),
-  // H = b ^ c ^ d (0x96), I = c ^ (b | ~d) (0x39)
-  constexpr unsigned kTruth[4] = {0xCA, 0xE4, 0x96, 0x39};
-  const uint32_t f = __builtin_amdgcn_bitop3_b32(b, c, d, kTruth[q]);
-  constexpr int g = q == 0 ? R : q == 1 ? (5 * R + 1) & 15 : q == 2 ? (3 * R + 5) & 15 : (7 * R) & 15;
-  constexpr uint32_t kr = kMd5K[R];  // compile-time constant: no load
-  const uint32_t x = a + kr + m[g];    // off the critical path: a is 4 rounds old
-  a = b + rotl(f + x, kShift[q][R & 3]);
-}
-
-template <int... Rs>
-__device__ __forceinline__ void md5_rounds(uint32_t (&h)[4], const uint32_t (&m)[16], std::integer_sequence<int, Rs...>) {
-  // the four state words rotate roles every round: (a,b,c,d) -> (d,a,b,c)
-  uint32_t s[4] = {h[0], h[1], h[2], h[3]};
-  (..., [&] {
-    constexpr int ia = (64 - Rs) & 3, ib = (65 - Rs) & 3, ic = (66 - Rs) & 3, id = (67 - Rs) & 3;
-    md5_round<Rs>(s[ia], s[ib], s[ic], s[id], m);
-  }());
-  h[0] += s[0];
-  h[1] += s[1];
-  h[2] += s[2];
-  h[3] += s[3];
-}
-
-__device__ __forceinline__ void md5_block(uint32_t (&h)[4], const uint32_t (&m)[16]) {
-  md5_rounds(h, m, std::make_integer_sequence<int, 64>{});
-}
+using dev::md5_block;
+using dev::u32x4;
 
 template <bool NT>
 __device__ __forceinline__ void load_block(const uint8_t *p, uint32_t (&m)[16]) {

@@ -710,8 +710,28 @@ int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_obj
   nxec_gf_gen_rs_matrix(enc.data(), n, k);
   const uint8_t *prow = enc.data() + static_cast<size_t>(k) * k;
   // full stripes: data chunks are read in place from the object (no copy of
-  // rs.cc:80), parity chunk (s, i) at d_parity + (s*p + i)*M
-  if (nf > 0 && p > 0) {
+  // rs.cc:80), parity chunk (s, i) at d_parity + (s*p + i)*M; with digests
+  // wanted, the encode and the MD5 of all n chunks run as one kernel
+  const int64_t ds = int64_t(n) * 16;
+  const bool fused = d_md5 && nf > 0 && encode_md5_eligible(k, p, M, d_object, M, k * M, d_parity, M, p * M);
+  if (fused) {
+    EncMd5Args ea{};
+    ea.data = d_object;
+    ea.data_chunk_stride = M;
+    ea.data_stripe_stride = k * M;
+    ea.parity = d_parity;
+    ea.parity_chunk_stride = M;
+    ea.parity_stripe_stride = p * M;
+    ea.digests = d_md5;
+    ea.digest_stripe_stride = ds;
+    ea.len = M;
+    ea.nstripes = nf;
+    ea.k = k;
+    ea.p = p;
+    std::memcpy(ea.coef, prow, static_cast<size_t>(p) * k);
+    rc = launch_encode_md5(ea, ctx->num_cus, st);
+    if (rc) return rc;
+  } else if (nf > 0 && p > 0) {
     rc = nxec_stripes_mul(ctx, p, k, prow, d_object, nullptr, M, k * M, d_parity, nullptr, M, p * M, nullptr, M, nf,
                           st);
     if (rc) return rc;
@@ -729,11 +749,12 @@ int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_obj
   }
   if (!d_md5) return NXEC_OK;
   // per-chunk MD5 (writeFileStripe -> Chunk::computeMD5, chunk_manager.cc:175): one launch over
-  // full-stripe data, full-stripe parity, tail data, tail parity; digests [s][n][16]
-  const int64_t ds = int64_t(n) * 16;
+  // full-stripe data, full-stripe parity, tail data, tail parity; digests
+  // [s][n][16] (the full stripes' are done when the fused kernel ran)
+  const int64_t nfm = fused ? 0 : nf;
   const Md5Region r[4] = {
-      {d_object, M, k * M, M, nf, d_md5, ds, k},
-      {d_parity, M, p * M, M, nf, d_md5 + int64_t(k) * 16, ds, p},
+      {d_object, M, k * M, M, nfm, d_md5, ds, k},
+      {d_parity, M, p * M, M, nfm, d_md5 + int64_t(k) * 16, ds, p},
       {d_tail, cs_last, k * cs_last, cs_last, tail ? 1 : 0, d_md5 + nf * ds, ds, k},
       {d_parity + nf * p * M, M, p * M, cs_last, tail ? 1 : 0, d_md5 + nf * ds + int64_t(k) * 16, ds, p},
   };

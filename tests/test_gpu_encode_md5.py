@@ -1,0 +1,134 @@
+"""Fused encode + per-chunk MD5 (k_encode_md5, nexoedge_amd/csrc/nxec_encode_md5.hip).
+
+The proxy's write path (chunk_manager.cc:66-452) codes each stripe with
+RSCode::encode and then hashes every chunk (Chunk::computeMD5, :175).  The
+fused kernel does both in one pass; bar: parity bit-exact with the oracle
+(the reference's ISA-L arithmetic), digests equal to hashlib's MD5, and both
+byte-identical to the two-kernel path (NXEC_FUSED_MD5=0) on the same inputs.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import fill_bytes
+from nexoedge_amd import nxec
+
+pytestmark = pytest.mark.gpu
+
+
+def _encode_object(ctx, n, k, M, obj_buf, length, fused):
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    p = n - k
+    par = nxec.DeviceBuffer(max(ns * p * M, 1))
+    tail = nxec.DeviceBuffer(k * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16 + 3)
+    old = os.environ.get("NXEC_FUSED_MD5")
+    os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
+    try:
+        # digests at an odd address: the kernel writes them byte-wise
+        ctx.encode_object(n, k, obj_buf.ptr, length, M, par.ptr, tail.ptr, md5.ptr + 3)
+        ctx.sync()
+    finally:
+        if old is None:
+            del os.environ["NXEC_FUSED_MD5"]
+        else:
+            os.environ["NXEC_FUSED_MD5"] = old
+    out = par.download().reshape(ns, p, M), md5.download()[3:].reshape(ns, n, 16)
+    for b in (par, tail, md5):
+        b.free()
+    return out
+
+
+@pytest.mark.parametrize("n,k,M,nstripes", [
+    (14, 10, 256, 1),        # one step, one stripe
+    (14, 10, 4096, 37),      # groups of 16 stripes + a partial group
+    (5, 4, 256, 300),        # p = 1, many groups
+    (6, 4, 65536, 17),       # config-1 geometry, 256 steps
+    (24, 20, 512, 13),       # k = 20, p = 4: S = 10 stripes per group, one LDS table copy
+    (16, 12, 1024, 21),      # k = 12: largest k with two table copies
+    (17, 13, 768, 33),       # k = 13, chunk an odd multiple of the step
+    (3, 1, 256, 40),         # k = 1
+    (9, 7, 2048, 5),         # fewer stripes than CUs x S: S shrinks
+])
+def test_fused_encode_md5_matches_oracle_and_hashlib(gpu_ctx, n, k, M, nstripes):
+    length = nstripes * k * M  # full stripes only: all of them through the fused kernel
+    obj = fill_bytes(length, 9100 + n * 31 + M)
+    ob = nxec.DeviceBuffer(length)
+    ob.upload(obj)
+    par, dig = _encode_object(gpu_ctx, n, k, M, ob, length, fused=True)
+    par2, dig2 = _encode_object(gpu_ctx, n, k, M, ob, length, fused=False)
+    ob.free()
+    assert np.array_equal(par, par2)
+    assert np.array_equal(dig, dig2)
+    p = n - k
+    for s in sorted({0, nstripes // 2, nstripes - 1}):
+        st = oracle.rs_encode(n, k, obj[s * k * M:(s + 1) * k * M], M)
+        for i in range(p):
+            assert np.array_equal(par[s, i], st[k + i]), (s, i)
+        for c in range(n):
+            assert dig[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
+
+
+def test_fused_encode_md5_object_with_tail(gpu_ctx):
+    """Full stripes through the fused kernel, the zero-padded last stripe
+    (chunk_manager.cc:390-399) through encode + MD5: every digest vs hashlib."""
+    n, k, M = 14, 10, 8192
+    length = 5 * k * M + 12345
+    obj = fill_bytes(length, 4242)
+    ob = nxec.DeviceBuffer(length)
+    ob.upload(obj)
+    par, dig = _encode_object(gpu_ctx, n, k, M, ob, length, fused=True)
+    ob.free()
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    assert (ns, nf) == (6, 5)
+    for s in range(ns):
+        cs = M if s < nf else cl
+        sd = np.zeros(k * cs, dtype=np.uint8)
+        piece = obj[s * k * M:s * k * M + k * cs]
+        sd[:len(piece)] = piece
+        st = oracle.rs_encode(n, k, sd, cs)
+        for i in range(n - k):
+            assert np.array_equal(par[s, i, :cs], st[k + i])
+        for c in range(n):
+            assert dig[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
+
+
+def test_fused_encode_md5_full_batch(gpu_ctx):
+    """BASELINE size: 4096 RS(10,4) stripes of 1 MiB (56 GiB).  Fused parity and
+    all 57 344 digests equal the two-kernel path's (whose digests
+    test_rs10_4_full_batch_roundtrip pins to hashlib stripe by stripe); three
+    stripes re-checked against the oracle and hashlib here."""
+    n, k, M, ns = 14, 10, 1 << 20, 4096
+    p = n - k
+    length = ns * k * M
+    ob = nxec.DeviceBuffer(length)
+    ob.fill_random(321)
+    par = nxec.DeviceBuffer(ns * p * M)
+    dig = [nxec.DeviceBuffer(ns * n * 16) for _ in range(2)]
+    sums = []
+    for fused in (True, False):
+        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
+        try:
+            par.memset(0)
+            gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, None, dig[0 if fused else 1].ptr)
+            gpu_ctx.sync()
+        finally:
+            del os.environ["NXEC_FUSED_MD5"]
+        sums.append(par.checksum())
+    assert sums[0] == sums[1]
+    d0 = dig[0].download().reshape(ns, n, 16)
+    d1 = dig[1].download().reshape(ns, n, 16)
+    assert np.array_equal(d0, d1)
+    for s in (0, 1777, ns - 1):
+        data = ob.download(k * M, offset=s * k * M)
+        st = oracle.rs_encode(n, k, data, M)
+        pp = par.download(p * M, offset=s * p * M).reshape(p, M)
+        for i in range(p):
+            assert np.array_equal(pp[i], st[k + i])
+        for c in range(n):
+            assert d0[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
+    for b in [ob, par] + dig:
+        b.free()
