@@ -208,6 +208,8 @@ PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file
     ("mixed16", 4 << 20, "auto"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
     ("mixed16", 4 << 20, "recover"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
     ("mixed16", 4 << 20, "natural"): ("r02_pmc_mixed16_4m_packed.json", "encode"),
+    ("write14", 1 << 20, "auto"): ("r02_pmc_write14_fused.json", "encode_md5_fused"),
+    ("write14", 1 << 20, "natural"): ("r02_pmc_write14_fused.json", "encode_md5_fused"),
     ("repair12", 1 << 20, "natural"): ("r02_pmc_repair12.json", "repair_fused_perm12"),
     ("repair12", 1 << 20, "auto"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
     ("repair12", 1 << 20, "recover"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
@@ -329,23 +331,27 @@ def wl_mixed16(args, ctx, stream, rank):
 
 def wl_write14(args, ctx, stream, rank):
     """Write path of the proxy (chunk_manager.cc:99-175): RS(10,4) encode of the
-    batch, then the MD5 digest of all n chunks of every stripe (Chunk::computeMD5,
-    chunk.hh:136).  MD5 is a serial chain per chunk, so its kernel runs one lane
-    per chunk and is ALU-bound, not HBM-bound."""
+    batch plus the MD5 digest of all n chunks of every stripe (Chunk::computeMD5,
+    chunk.hh:136), as ONE fused kernel (nxec_rs_encode_md5_stripes ->
+    k_encode_md5): the data is read from HBM once, the parity written once, and
+    every chunk's MD5 chain runs on the same bytes from LDS.  MD5 is a serial
+    chain per chunk (one lane each), so the kernel is bound by the chain's VALU
+    issue, not by HBM."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
     stripe = n * cs
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xC0FFEE + rank * 7919)
     dig = nxec.DeviceBuffer(ns * n * 16)
     ops = [
-        ("encode", lambda i: ctx.rs_encode(n, k, buf.ptr, cs, stripe, cs, ns, stream), ns * n * cs),
-        ("md5_all_chunks", lambda i: ctx.md5_chunks(buf.ptr, cs, stripe, n, cs, ns, dig.ptr, stream), ns * n * cs),
+        ("encode_md5_fused", lambda i: ctx.rs_encode_md5(n, k, buf.ptr, cs, stripe, cs, ns, dig.ptr, stream),
+         ns * n * cs),
     ]
-    config = {"workload": f"RS({n},{k}) write path: encode + per-chunk MD5 of all {n} chunks, {cs >> 10} KiB chunks, "
-                          f"{ns} stripes per GPU", "stripes_per_gpu": ns, "chunk_bytes": cs,
-              "byte_accounting": "encode n*cs + md5 n*cs per stripe"}
+    config = {"workload": f"RS({n},{k}) write path: encode + per-chunk MD5 of all {n} chunks in one fused kernel, "
+                          f"{cs >> 10} KiB chunks, {ns} stripes per GPU", "stripes_per_gpu": ns, "chunk_bytes": cs,
+              "byte_accounting": "n*cs per stripe: one HBM pass (k*cs read, (n-k)*cs written); the MD5 of all n "
+                                 "chunks reads the same bytes from LDS"}
     return Workload("write14", "GiB/s RS(10,4) encode + per-chunk MD5, 1 MiB chunks, device-resident", config, ops,
-                    [buf, dig], f"k_mul_vec<K={k},R=8> work-queue (encode launch)", ns)
+                    [buf, dig], f"k_encode_md5<K={k}> (fused encode + MD5; MD5-chain-bound, not HBM-bound)", ns)
 
 
 def wl_object(args, ctx, stream, rank):
@@ -368,16 +374,17 @@ def wl_object(args, ctx, stream, rank):
     failed = list(range(min(4, p)))
     ops = [
         ("write_encode_object_md5", lambda i: ctx.encode_object(n, k, obj.ptr, length, M, par.ptr, None, md5.ptr, stream),
-         2 * ns * n * M),
+         ns * n * M),
         ("read_decode_object", lambda i: ctx.decode_object(n, k, failed, chunks.ptr, length, M, out.ptr, None, stream),
          2 * ns * k * M),
     ]
     config = {"workload": f"object of {ns} RS({n},{k}) stripes ({length >> 30} GiB), {M >> 10} KiB chunks: write = "
                           f"encode_object + MD5 of all chunks, read = decode_object with chunks {failed} lost",
               "stripes_per_gpu": ns, "chunk_bytes": M,
-              "byte_accounting": "write: encode n*cs + MD5 n*cs per stripe; read: full-output decode 2k*cs per stripe"}
+              "byte_accounting": "write: n*cs per stripe (one fused encode + MD5 pass); read: full-output decode "
+                                 "2k*cs per stripe"}
     return Workload("object", "GiB/s object write (encode+MD5) + read (decode), RS(10,4), 1 MiB chunks, device-resident",
-                    config, ops, [obj, par, md5, chunks, out], "encode_object (encode + MD5 launches)", ns)
+                    config, ops, [obj, par, md5, chunks, out], "encode_object (fused k_encode_md5)", ns)
 
 
 def wl_files(args, ctx, stream, rank):

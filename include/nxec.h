@@ -242,6 +242,16 @@ int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t
                            int nchunks, int64_t len, int64_t nstripes, const unsigned char *d_expected,
                            unsigned char *d_ok, unsigned long long *d_nbad, void *stream);
 
+/* RSCode::encode plus Chunk::computeMD5 of all n chunks of every stripe of a
+ * device-resident batch -- the write path's coding work (chunk_manager.cc:
+ * 99-175) -- in one pass over the data: parity as nxec_rs_encode_stripes,
+ * digests as nxec_md5_chunks (d_digests[(s*n + c)*16]).  One fused kernel
+ * when n - k <= 4, k <= 20, len is a multiple of 256 and the layout is 16-byte
+ * aligned; otherwise the encode, then the MD5 launch. */
+int nxec_rs_encode_md5_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_stripes, int64_t chunk_stride,
+                               int64_t stripe_stride, int64_t len, int64_t nstripes, unsigned char *d_digests,
+                               void *stream);
+
 /* ---- Object-level batched entry (ChunkManager write/read of a
  * whole object in one call instead of the per-stripe loop of
  * proxy_file_ops.cc:557-666 / chunk_manager.cc:99,787).

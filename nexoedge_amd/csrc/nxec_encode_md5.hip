@@ -45,7 +45,6 @@ namespace {
 
 using dev::build_tables;
 using dev::ld_stream;
-using dev::lookup16;
 using dev::md5_block;
 using dev::md5_init;
 using dev::md5_pad_aligned;
@@ -62,10 +61,48 @@ constexpr int kEmMaxStripes = kEmCodeLanes / kEmVecs;
 constexpr int kEmLds = 160 * 1024;
 constexpr int kEmBufMax = 2 * kEmMaxRows * kEmRow;
 
-// table replication: 2 copies where they fit beside two full buffers
-template <int K>
-constexpr int em_r() {
-  return kEmBufMax + K * 1024 * 2 <= kEmLds ? 2 : 1;
+// Byte b of w times 4 (its table entry's byte offset) in one VALU op: an SDWA
+// source select instead of v_bfe + v_lshl_add.  Not volatile: the compiler
+// schedules these freely.
+template <int B>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t w) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w));
+  else if constexpr (B == 1)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w));
+  else if constexpr (B == 2)
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w));
+  else
+    asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w));
+  return r;
+}
+
+// acc[4q + b] ^= T_j0[byte b of word q of d0] ^ T_j1[... of d1] over the
+// single-copy tables at LDS byte 0 (entry x of source j at j*1024 + 4x):
+// one SDWA address op per byte, the source's table offset as the ds_read
+// immediate, one v_bitop3 (3-way XOR) per two lookups.  The tables are the
+// first bytes of the dynamic LDS and the kernel has no static LDS
+// (prepare_encode_md5 checks), so an integer LDS address is the table offset.
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+__device__ __forceinline__ uint32_t ent(int table_off, uint32_t byte_off) {
+  return *reinterpret_cast<lds_u32 *>(static_cast<uintptr_t>(byte_off + table_off));
+}
+__device__ __forceinline__ void lookup_pair(int j0, bool two, const u32x4 d0, const u32x4 d1, uint32_t acc[16]) {
+  const uint32_t w0[4] = {d0.x, d0.y, d0.z, d0.w}, w1[4] = {d1.x, d1.y, d1.z, d1.w};
+  const int t0 = j0 * 1024, t1 = t0 + 1024;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t a[4] = {byte_x4<0>(w0[q]), byte_x4<1>(w0[q]), byte_x4<2>(w0[q]), byte_x4<3>(w0[q])};
+    if (two) {  // constant after unrolling
+      const uint32_t b[4] = {byte_x4<0>(w1[q]), byte_x4<1>(w1[q]), byte_x4<2>(w1[q]), byte_x4<3>(w1[q])};
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[4 * q + i] = __builtin_amdgcn_bitop3_b32(acc[4 * q + i], ent(t0, a[i]), ent(t1, b[i]), 0x96);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[4 * q + i] ^= ent(t0, a[i]);
+    }
+  }
 }
 
 // prefetch ring depth: as many 4K-VGPR source buffers as fit in ~170 VGPRs
@@ -85,14 +122,13 @@ __device__ __forceinline__ void lds_barrier() {
 // the table lookups (parity = first source), to time each role alone.
 template <int K, int PROBE = 0>
 __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
-  constexpr int R = em_r<K>();
   extern __shared__ __align__(16) uint8_t lds[];
   const int n = K + a.p;
   const int S = a.stripes_per_group;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
-  uint8_t *buf = lds + K * 1024 * R;
+  uint8_t *buf = lds + K * 1024;
   const uint32_t buf_bytes = static_cast<uint32_t>(S * n * kEmRow);
-  build_tables<R>(a.coef, K, a.p, tab);
+  build_tables<1>(a.coef, K, a.p, tab);
   __syncthreads();
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
   const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
@@ -109,7 +145,6 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
     const uint8_t *src = a.data + (s0 + ls) * a.data_stripe_stride + v * 16;
     uint8_t *dst = a.parity + (s0 + ls) * a.parity_stripe_stride + v * 16;
     uint8_t *row = buf + ls * n * kEmRow + v * 16;
-    const char *tl = reinterpret_cast<const char *>(tab) + (threadIdx.x % R) * 4;
     auto load = [&](int step, u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
 #pragma unroll
@@ -121,15 +156,16 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = 0;
 #pragma unroll
-      for (int j = 0; j < K; j++) {
+      for (int j = 0; j < K; j += 2) {
         *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+        if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
         if (PROBE & 2) {
           if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
         } else {
-          lookup16<R>(tl + j * 1024 * R, d[j], acc);
+          lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
         }
-        // materialise the accumulators per source: left alone, LLVM turns
-        // the XOR chains into trees over all k sources, which keeps 16
+        // materialise the accumulators per source pair: left alone, LLVM
+        // turns the XOR chains into trees over all k sources, which keeps 16
         // lookup results per source live at once (spills from k = 10)
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
@@ -255,8 +291,6 @@ const std::array<EmKernel, kEncMd5MaxK> kEm = em_table(std::make_integer_sequenc
 
 const EmKernel kEmProbe[4] = {&k_encode_md5<10, 0>, &k_encode_md5<10, 1>, &k_encode_md5<10, 2>, &k_encode_md5<10, 3>};
 
-int em_r_of(int k) { return 2 * kEmMaxRows * kEmRow + k * 1024 * 2 <= kEmLds ? 2 : 1; }
-
 }  // namespace
 
 bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t data_cs, int64_t data_ss,
@@ -273,6 +307,9 @@ bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t da
 
 int prepare_encode_md5() {
   for (int k = 1; k <= kEncMd5MaxK; k++) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kEm[k - 1])) != hipSuccess || fa.sharedSizeBytes != 0)
+      return set_error(NXEC_ERR_HIP, "k_encode_md5: static LDS present (the tables must start at LDS byte 0)");
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEm[k - 1]),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_encode_md5): %s", hipGetErrorString(e));
@@ -299,7 +336,7 @@ int launch_encode_md5(const EncMd5Args &in, int num_cus, void *stream) {
   if (const char *e = std::getenv("NXEC_EM_PRIO")) a.hash_prio = std::atoi(e);
   const int64_t grid = (a.nstripes + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
-  const int lds = a.k * 1024 * em_r_of(a.k) + static_cast<int>(2 * S * n * kEmRow);
+  const int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.k - 1];
   if (const char *e = std::getenv("NXEC_EM_PROBE"))
     if (a.k == 10) fn = kEmProbe[std::atoi(e) & 3];

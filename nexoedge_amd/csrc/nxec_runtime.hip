@@ -659,6 +659,41 @@ int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t
   return launch_md5(&r, 1, pick_stream(ctx, stream), d_ok, d_nbad);
 }
 
+int nxec_rs_encode_md5_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_stripes, int64_t chunk_stride,
+                               int64_t stripe_stride, int64_t len, int64_t nstripes, unsigned char *d_digests,
+                               void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
+  if (len < 0 || nstripes < 0 || ((len > 0 && nstripes > 0) && (!d_stripes || !d_digests)))
+    return set_error(NXEC_ERR_INVALID, "nxec_rs_encode_md5_stripes: invalid arguments");
+  if (nstripes == 0) return NXEC_OK;
+  const int p = n - k;
+  unsigned char *d_par = d_stripes + int64_t(k) * chunk_stride;
+  if (encode_md5_eligible(k, p, len, d_stripes, chunk_stride, stripe_stride, d_par, chunk_stride, stripe_stride)) {
+    int rc = ensure_device(ctx->device);
+    if (rc) return rc;
+    std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+    nxec_gf_gen_rs_matrix(enc.data(), n, k);  // rs.cc:26
+    EncMd5Args ea{};
+    ea.data = d_stripes;
+    ea.data_chunk_stride = chunk_stride;
+    ea.data_stripe_stride = stripe_stride;
+    ea.parity = d_par;
+    ea.parity_chunk_stride = chunk_stride;
+    ea.parity_stripe_stride = stripe_stride;
+    ea.digests = d_digests;
+    ea.digest_stripe_stride = int64_t(n) * 16;
+    ea.len = len;
+    ea.nstripes = nstripes;
+    ea.k = k;
+    ea.p = p;
+    std::memcpy(ea.coef, enc.data() + static_cast<size_t>(k) * k, static_cast<size_t>(p) * k);
+    return launch_encode_md5(ea, ctx->num_cus, pick_stream(ctx, stream));
+  }
+  int rc = nxec_rs_encode_stripes(ctx, n, k, d_stripes, chunk_stride, stripe_stride, len, nstripes, stream);
+  return rc ? rc : nxec_md5_chunks(ctx, d_stripes, chunk_stride, stripe_stride, n, len, nstripes, d_digests, stream);
+}
+
 int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride) {
   if (n < 1 || n > NXEC_MAX_N || len < 0 || !chunk_stride || !stripe_stride)
     return set_error(NXEC_ERR_INVALID, "nxec_batch_layout: invalid arguments");

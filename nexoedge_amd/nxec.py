@@ -355,6 +355,13 @@ class Context:
         check(lib.nxec_md5_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride, nchunks,
                                   length, nstripes, C.c_void_p(int(digests)), stream), "nxec_md5_chunks")
 
+    def rs_encode_md5(self, n: int, k: int, stripes: int, chunk_stride: int, stripe_stride: int, length: int,
+                      nstripes: int, digests: int, stream=None) -> None:
+        """nxec_rs_encode_md5_stripes: parity + MD5 of all n chunks per stripe (digests [s][n][16])."""
+        check(lib.nxec_rs_encode_md5_stripes(C.c_void_p(self.ptr), n, k, C.c_void_p(int(stripes)), chunk_stride,
+                                             stripe_stride, length, nstripes, C.c_void_p(int(digests)), stream),
+              "nxec_rs_encode_md5_stripes")
+
     def md5_verify_chunks(self, base: int, chunk_stride: int, stripe_stride: int, nchunks: int, length: int,
                           nstripes: int, expected: int, ok: int, nbad=None, stream=None) -> None:
         check(lib.nxec_md5_verify_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride,

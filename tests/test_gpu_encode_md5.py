@@ -132,3 +132,40 @@ def test_fused_encode_md5_full_batch(gpu_ctx):
             assert d0[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
     for b in [ob, par] + dig:
         b.free()
+
+
+@pytest.mark.parametrize("n,k,cs,cstride,sstride,ns", [
+    (14, 10, 65536, 65536, 14 * 65536, 40),              # packed [s][n][cs]
+    (14, 10, 65536, 65536 + 2048, 15 * (65536 + 2048), 33),  # padded chunk and stripe strides
+    (20, 16, 4096, 4096 + 16, 21 * (4096 + 16), 300),    # RS(16,4), odd stride padding
+    (6, 4, 1000, 1008, 6 * 1008, 9),                     # len not a multiple of 256: encode + MD5 launches
+])
+def test_rs_encode_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns):
+    """nxec_rs_encode_md5_stripes == nxec_rs_encode_stripes + nxec_md5_chunks on the
+    same batch; sampled stripes vs the oracle and hashlib."""
+    host = np.zeros((ns, sstride), dtype=np.uint8)
+    data = fill_bytes(ns * k * cs, 77 + cs).reshape(ns, k, cs)
+    for s in range(ns):
+        for j in range(k):
+            host[s, j * cstride:j * cstride + cs] = data[s, j]
+    a = nxec.DeviceBuffer(host.nbytes)
+    b = nxec.DeviceBuffer(host.nbytes)
+    a.upload(host)
+    b.upload(host)
+    da = nxec.DeviceBuffer(ns * n * 16)
+    db = nxec.DeviceBuffer(ns * n * 16)
+    gpu_ctx.rs_encode_md5(n, k, a.ptr, cstride, sstride, cs, ns, da.ptr)
+    gpu_ctx.rs_encode(n, k, b.ptr, cstride, sstride, cs, ns)
+    gpu_ctx.md5_chunks(b.ptr, cstride, sstride, n, cs, ns, db.ptr)
+    gpu_ctx.sync()
+    ha, hb = a.download().reshape(ns, sstride), b.download().reshape(ns, sstride)
+    assert np.array_equal(ha, hb)
+    ga, gb = da.download().reshape(ns, n, 16), db.download().reshape(ns, n, 16)
+    assert np.array_equal(ga, gb)
+    for s in sorted({0, ns // 3, ns - 1}):
+        st = oracle.rs_encode(n, k, data[s].reshape(-1), cs)
+        for c in range(n):
+            assert np.array_equal(ha[s, c * cstride:c * cstride + cs], st[c]), (s, c)
+            assert ga[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
+    for x in (a, b, da, db):
+        x.free()
