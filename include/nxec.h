@@ -252,6 +252,17 @@ int nxec_rs_encode_md5_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_s
                                int64_t stripe_stride, int64_t len, int64_t nstripes, unsigned char *d_digests,
                                void *stream);
 
+/* Repair with checksums: nxec_rs_recover_stripes (rebuilds the `nfailed`
+ * chunks in place from the first k alive ones, rs.cc:238-322) plus the MD5 of
+ * every rebuilt chunk -- the proxy's repair step before it sends the chunks
+ * out (chunk_manager.cc:1173, Chunk::computeMD5) -- in one pass.  Digest of
+ * rebuilt chunk failed[r] of stripe s at d_digests[(s*nfailed + r)*16].  One
+ * fused kernel when nfailed <= 4, k <= 20, len is a multiple of 256 and the
+ * layout is 16-byte aligned; otherwise the recover, then the MD5 launch. */
+int nxec_rs_recover_md5_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                                unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride, int64_t len,
+                                int64_t nstripes, unsigned char *d_digests, void *stream);
+
 /* ---- Object-level batched entry (ChunkManager write/read of a
  * whole object in one call instead of the per-stripe loop of
  * proxy_file_ops.cc:557-666 / chunk_manager.cc:99,787).

@@ -1,4 +1,7 @@
-// Fused RS encode + per-chunk MD5 of a stripe batch on gfx950.
+// Fused GF(2^8) multiply + per-chunk MD5 of a stripe batch on gfx950
+// (SURVEY §8f.1-f.2): the write path's encode + MD5 of all n chunks, and the
+// repair path's recover + MD5 of the rebuilt chunks (chunk_manager.cc:1173).
+// Described below for the write path (the harder case: every chunk hashed).
 //
 // The proxy's write path codes every stripe and then hashes every chunk it
 // sends (chunk_manager.cc:66-452: RSCode::encode, then Chunk::computeMD5 at
@@ -59,7 +62,6 @@ constexpr int kEmRow = kEncMd5Step + 16;       // LDS row stride: bank rotation 
 constexpr int kEmMaxRows = 256;                // chunks per workgroup = hash lanes
 constexpr int kEmMaxStripes = kEmCodeLanes / kEmVecs;
 constexpr int kEmLds = 160 * 1024;
-constexpr int kEmBufMax = 2 * kEmMaxRows * kEmRow;
 
 // Byte b of w times 4 (its table entry's byte offset) in one VALU op: an SDWA
 // source select instead of v_bfe + v_lshl_add.  Not volatile: the compiler
@@ -121,13 +123,14 @@ __device__ __forceinline__ void lds_barrier() {
 // bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
 // the table lookups (parity = first source), to time each role alone.
 template <int K, int PROBE = 0>
-__global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
+__global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int n = K + a.p;
+  const int nh = a.nhashed;  // hashed chunks per stripe: LDS rows per stripe
+  const int hsrc = a.hash_src ? K : 0;  // rows before the outputs' rows
   const int S = a.stripes_per_group;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
-  const uint32_t buf_bytes = static_cast<uint32_t>(S * n * kEmRow);
+  const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
   build_tables<1>(a.coef, K, a.p, tab);
   __syncthreads();
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
@@ -142,13 +145,13 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
     // and waits only for the ring slot it consumes.
     const int item = threadIdx.x;
     const int ls = item < nS * kEmVecs ? item / kEmVecs : 0, v = item % kEmVecs;
-    const uint8_t *src = a.data + (s0 + ls) * a.data_stripe_stride + v * 16;
-    uint8_t *dst = a.parity + (s0 + ls) * a.parity_stripe_stride + v * 16;
-    uint8_t *row = buf + ls * n * kEmRow + v * 16;
+    const uint8_t *src = a.src + (s0 + ls) * a.src_stripe_stride + v * 16;
+    uint8_t *dst = a.dst + (s0 + ls) * a.dst_stripe_stride + v * 16;
+    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
     auto load = [&](int step, u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
 #pragma unroll
-      for (int j = 0; j < K; j++) d[j] = ld_stream(src + j * a.data_chunk_stride + off);
+      for (int j = 0; j < K; j++) d[j] = ld_stream(src + a.src_off[j] + off);
     };
     auto run = [&](int step, const u32x4(&d)[K]) {
       uint8_t *rb = row + (step & 1) * buf_bytes;
@@ -157,8 +160,10 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
       for (int i = 0; i < 16; i++) acc[i] = 0;
 #pragma unroll
       for (int j = 0; j < K; j += 2) {
-        *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
-        if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
+        if (hsrc) {  // wave-uniform
+          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
+        }
         if (PROBE & 2) {
           if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
         } else {
@@ -177,8 +182,8 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          st_stream(dst + r * a.parity_chunk_stride + off, pv);
-          *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = pv;
+          st_stream(dst + a.dst_off[r] + off, pv);
+          if (a.hash_dst) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;
         }
       }
       lds_barrier();  // this step's buffer is full
@@ -215,10 +220,10 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
     return;
   }
 
-  // ---- hash waves: lane h = chunk (h / n, h % n) of the group = LDS row h ----
+  // ---- hash waves: lane h = hashed chunk (h / nh, h % nh) of the group = LDS row h ----
   if (a.hash_prio) __builtin_amdgcn_s_setprio(1);
   const int h = threadIdx.x - kEmCodeLanes;
-  const bool active = h < nS * n;
+  const bool active = h < nS * nh;
   const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
   uint32_t st[4];
   md5_init(st);
@@ -275,33 +280,34 @@ __global__ __launch_bounds__(kEmBlock) void k_encode_md5(const EncMd5Args a) {
   }
   if (active) {
     md5_pad_aligned(st, static_cast<uint64_t>(a.len));
-    const int ls = h / n, c = h - ls * n;
-    uint8_t *out = a.digests + (s0 + ls) * a.digest_stripe_stride + c * 16;
+    const int ls = h / nh, c = h - ls * nh;
+    uint8_t *out = a.digests + (s0 + ls) * a.digest_stripe_stride + a.digest_slot[c] * 16;
 #pragma unroll
     for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
   }
 }
 
-using EmKernel = void (*)(const EncMd5Args);
+using EmKernel = void (*)(const MulMd5Args);
 template <int... Ks>
 constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int, Ks...>) {
-  return {{&k_encode_md5<Ks + 1>...}};
+  return {{&k_mul_md5<Ks + 1>...}};
 }
 const std::array<EmKernel, kEncMd5MaxK> kEm = em_table(std::make_integer_sequence<int, kEncMd5MaxK>{});
 
-const EmKernel kEmProbe[4] = {&k_encode_md5<10, 0>, &k_encode_md5<10, 1>, &k_encode_md5<10, 2>, &k_encode_md5<10, 3>};
+const EmKernel kEmProbe[4] = {&k_mul_md5<10, 0>, &k_mul_md5<10, 1>, &k_mul_md5<10, 2>, &k_mul_md5<10, 3>};
 
 }  // namespace
 
-bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t data_cs, int64_t data_ss,
-                         const void *parity, int64_t parity_cs, int64_t parity_ss) {
-  if (k < 1 || k > kEncMd5MaxK || p < 1 || p > kMaxRowsPerPass) return false;
+bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src_stripe_stride, const uint32_t *src_off,
+                     const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off) {
+  if (k < 1 || k > kEncMd5MaxK || rows < 1 || rows > kMaxRowsPerPass) return false;
   if (len <= 0 || len % kEncMd5Step != 0 || len / kEncMd5Step >= (int64_t(1) << 31)) return false;
   if (const char *e = std::getenv("NXEC_FUSED_MD5"))
-    if (e[0] == '0') return false;  // A/B: two kernels (encode, then MD5)
-  const uint64_t bits = reinterpret_cast<uintptr_t>(data) | reinterpret_cast<uintptr_t>(parity) |
-                        static_cast<uint64_t>(data_cs) | static_cast<uint64_t>(data_ss) |
-                        static_cast<uint64_t>(parity_cs) | static_cast<uint64_t>(parity_ss);
+    if (e[0] == '0') return false;  // A/B: two kernels (coding, then MD5)
+  uint64_t bits = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                  static_cast<uint64_t>(src_stripe_stride) | static_cast<uint64_t>(dst_stripe_stride);
+  for (int j = 0; j < k; j++) bits |= src_off[j];
+  for (int r = 0; r < rows; r++) bits |= dst_off[r];
   return (bits & 15) == 0;
 }
 
@@ -309,26 +315,28 @@ int prepare_encode_md5() {
   for (int k = 1; k <= kEncMd5MaxK; k++) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kEm[k - 1])) != hipSuccess || fa.sharedSizeBytes != 0)
-      return set_error(NXEC_ERR_HIP, "k_encode_md5: static LDS present (the tables must start at LDS byte 0)");
+      return set_error(NXEC_ERR_HIP, "k_mul_md5: static LDS present (the tables must start at LDS byte 0)");
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEm[k - 1]),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
-    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_encode_md5): %s", hipGetErrorString(e));
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5): %s", hipGetErrorString(e));
   }
   for (EmKernel fn : kEmProbe) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
-    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_encode_md5 probe): %s", hipGetErrorString(e));
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 probe): %s", hipGetErrorString(e));
   }
   return NXEC_OK;
 }
 
-int launch_encode_md5(const EncMd5Args &in, int num_cus, void *stream) {
+int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   if (in.nstripes <= 0) return NXEC_OK;
-  EncMd5Args a = in;
-  const int n = a.k + a.p;
+  MulMd5Args a = in;
+  a.nhashed = (a.hash_src ? a.k : 0) + (a.hash_dst ? a.p : 0);
+  if (a.nhashed < 1) return set_error(NXEC_ERR_INVALID, "mul+md5: nothing to hash");
+  const int n = a.nhashed;
   // as many stripes per workgroup as its 256 hash lanes and code lanes hold,
   // but spread over every CU first (each chain is ~9 ms of one lane whatever
   // the batch: fewer stripes per CU means shorter code steps, not shorter chains)
-  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / n);
+  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / n);  // n: hashed chunks per stripe
   const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
   if (per_cu < S) S = per_cu;
   a.stripes_per_group = static_cast<int32_t>(S);
@@ -343,7 +351,7 @@ int launch_encode_md5(const EncMd5Args &in, int num_cus, void *stream) {
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
-  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_encode_md5: %s", hipGetErrorString(e));
+  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_mul_md5: %s", hipGetErrorString(e));
 }
 
 }  // namespace nxec

@@ -144,32 +144,40 @@ struct Md5Item {
 };
 int launch_md5_list(const Md5Item *d_items, int64_t nitems, void *stream);
 
-// Fused encode + MD5 of every chunk (nxec_encode_md5.hip): parity row r of
-// stripe s at parity + s*parity_stripe_stride + r*parity_chunk_stride, data
-// chunk j at data + s*data_stripe_stride + j*data_chunk_stride; digest of
-// chunk c (data c < k, parity k + r) at digests + s*digest_stripe_stride + c*16.
-// Chunks are walked in steps of kEncMd5Step bytes (len a multiple of it).
+// Fused GF(2^8) multiply + MD5 (nxec_encode_md5.hip): per stripe s, output
+// row r (< rows <= 4) = XOR_j coef[r][j] * source j, source j at src +
+// s*src_stripe_stride + src_off[j], row r at dst + s*dst_stripe_stride +
+// dst_off[r]; the MD5 of every source (hash_src) and/or every output
+// (hash_dst) in the same pass, hashed chunk i (sources first) to digests +
+// s*digest_stripe_stride + digest_slot[i]*16.  Chunks are walked in steps of
+// kEncMd5Step bytes (len a multiple of it).  The write path (encode + MD5 of
+// all n chunks) and the repair path (recover + MD5 of the rebuilt chunks).
 constexpr int kEncMd5Step = 256;
 constexpr int kEncMd5MaxK = 20;
-struct EncMd5Args {
-  const uint8_t *data;
-  int64_t data_chunk_stride, data_stripe_stride;
-  uint8_t *parity;
-  int64_t parity_chunk_stride, parity_stripe_stride;
+struct MulMd5Args {
+  const uint8_t *src;
+  int64_t src_stripe_stride;
+  uint8_t *dst;
+  int64_t dst_stripe_stride;
   uint8_t *digests;
   int64_t digest_stripe_stride;
   int64_t len, nstripes;
-  int32_t k, p;
-  int32_t stripes_per_group;  // set by launch_encode_md5
-  int32_t hash_prio;          // hash waves at s_setprio 1 (set by launch_encode_md5)
+  int32_t k, p;                  // sources, output rows
+  int32_t hash_src, hash_dst;
+  int32_t nhashed;               // set by launch_mul_md5
+  int32_t stripes_per_group;     // set by launch_mul_md5
+  int32_t hash_prio;             // hash waves at s_setprio 1 (set by launch_mul_md5)
+  uint32_t src_off[NXEC_MAX_K + 1];
+  uint32_t dst_off[kMaxRowsPerPass];
+  uint8_t digest_slot[NXEC_MAX_K + 1 + kMaxRowsPerPass];
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
 };
-// k <= kEncMd5MaxK, 1 <= p <= 4, len a positive multiple of kEncMd5Step,
-// 16-byte aligned buffers and strides (NXEC_FUSED_MD5=0 disables, for A/B)
-bool encode_md5_eligible(int k, int p, int64_t len, const void *data, int64_t data_cs, int64_t data_ss,
-                         const void *parity, int64_t parity_cs, int64_t parity_ss);
+// k <= kEncMd5MaxK, 1 <= rows <= 4, len a positive multiple of kEncMd5Step,
+// 16-byte aligned buffers, strides and offsets (NXEC_FUSED_MD5=0 disables, for A/B)
+bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src_stripe_stride, const uint32_t *src_off,
+                      const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off);
 int prepare_encode_md5();
-int launch_encode_md5(const EncMd5Args &a, int num_cus, void *stream);
+int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 
 }  // namespace nxec
 

@@ -659,6 +659,45 @@ int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t
   return launch_md5(&r, 1, pick_stream(ctx, stream), d_ok, d_nbad);
 }
 
+}  // extern "C"
+
+namespace {
+
+// Fused write-path launch (encode + MD5 of all n chunks): data chunk j of
+// stripe s at data + s*data_ss + j*data_cs, parity row r at parity + s*par_ss
+// + r*par_cs, digests [s][n][16].  False when the fused kernel cannot take it.
+bool encode_md5_args(int n, int k, const unsigned char *data, int64_t data_cs, int64_t data_ss, unsigned char *parity,
+                     int64_t par_cs, int64_t par_ss, unsigned char *digests, int64_t len, int64_t nstripes,
+                     MulMd5Args &a) {
+  const int p = n - k;
+  if (k > kEncMd5MaxK || p < 1 || p > kMaxRowsPerPass) return false;
+  if (int64_t(k - 1) * data_cs >= (int64_t(1) << 32) || int64_t(p - 1) * par_cs >= (int64_t(1) << 32)) return false;
+  a = MulMd5Args{};
+  for (int j = 0; j < k; j++) a.src_off[j] = static_cast<uint32_t>(j * data_cs);
+  for (int r = 0; r < p; r++) a.dst_off[r] = static_cast<uint32_t>(r * par_cs);
+  if (!mul_md5_eligible(k, p, len, data, data_ss, a.src_off, parity, par_ss, a.dst_off)) return false;
+  std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
+  nxec_gf_gen_rs_matrix(enc.data(), n, k);  // rs.cc:26
+  std::memcpy(a.coef, enc.data() + static_cast<size_t>(k) * k, static_cast<size_t>(p) * k);
+  a.src = data;
+  a.src_stripe_stride = data_ss;
+  a.dst = parity;
+  a.dst_stripe_stride = par_ss;
+  a.digests = digests;
+  a.digest_stripe_stride = int64_t(n) * 16;
+  a.len = len;
+  a.nstripes = nstripes;
+  a.k = k;
+  a.p = p;
+  a.hash_src = a.hash_dst = 1;
+  for (int c = 0; c < n; c++) a.digest_slot[c] = static_cast<uint8_t>(c);
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
 int nxec_rs_encode_md5_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_stripes, int64_t chunk_stride,
                                int64_t stripe_stride, int64_t len, int64_t nstripes, unsigned char *d_digests,
                                void *stream) {
@@ -667,31 +706,68 @@ int nxec_rs_encode_md5_stripes(nxec_ctx_t *ctx, int n, int k, unsigned char *d_s
   if (len < 0 || nstripes < 0 || ((len > 0 && nstripes > 0) && (!d_stripes || !d_digests)))
     return set_error(NXEC_ERR_INVALID, "nxec_rs_encode_md5_stripes: invalid arguments");
   if (nstripes == 0) return NXEC_OK;
-  const int p = n - k;
-  unsigned char *d_par = d_stripes + int64_t(k) * chunk_stride;
-  if (encode_md5_eligible(k, p, len, d_stripes, chunk_stride, stripe_stride, d_par, chunk_stride, stripe_stride)) {
+  MulMd5Args ea;
+  if (encode_md5_args(n, k, d_stripes, chunk_stride, stripe_stride, d_stripes + int64_t(k) * chunk_stride, chunk_stride,
+                      stripe_stride, d_digests, len, nstripes, ea)) {
     int rc = ensure_device(ctx->device);
     if (rc) return rc;
-    std::vector<uint8_t> enc(static_cast<size_t>(n) * k);
-    nxec_gf_gen_rs_matrix(enc.data(), n, k);  // rs.cc:26
-    EncMd5Args ea{};
-    ea.data = d_stripes;
-    ea.data_chunk_stride = chunk_stride;
-    ea.data_stripe_stride = stripe_stride;
-    ea.parity = d_par;
-    ea.parity_chunk_stride = chunk_stride;
-    ea.parity_stripe_stride = stripe_stride;
-    ea.digests = d_digests;
-    ea.digest_stripe_stride = int64_t(n) * 16;
-    ea.len = len;
-    ea.nstripes = nstripes;
-    ea.k = k;
-    ea.p = p;
-    std::memcpy(ea.coef, enc.data() + static_cast<size_t>(k) * k, static_cast<size_t>(p) * k);
-    return launch_encode_md5(ea, ctx->num_cus, pick_stream(ctx, stream));
+    return launch_mul_md5(ea, ctx->num_cus, pick_stream(ctx, stream));
   }
   int rc = nxec_rs_encode_stripes(ctx, n, k, d_stripes, chunk_stride, stripe_stride, len, nstripes, stream);
   return rc ? rc : nxec_md5_chunks(ctx, d_stripes, chunk_stride, stripe_stride, n, len, nstripes, d_digests, stream);
+}
+
+int nxec_rs_recover_md5_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                                unsigned char *d_stripes, int64_t chunk_stride, int64_t stripe_stride, int64_t len,
+                                int64_t nstripes, unsigned char *d_digests, void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  if (!valid_nk(n, k)) return set_error(NXEC_ERR_INVALID, "invalid (n,k)=(%d,%d)", n, k);
+  if (nfailed < 0 || len < 0 || nstripes < 0 || (nfailed > 0 && !failed) ||
+      ((nfailed > 0 && len > 0 && nstripes > 0) && (!d_stripes || !d_digests)))
+    return set_error(NXEC_ERR_INVALID, "nxec_rs_recover_md5_stripes: invalid arguments");
+  if (nfailed == 0 || nstripes == 0) return NXEC_OK;
+  std::vector<int32_t> inputs(n);
+  std::vector<uint8_t> rm(static_cast<size_t>(nfailed) * k);
+  int ni = 0, mi = 0;
+  int rc = nxec_rs_plan(n, k, failed, nfailed, 1, inputs.data(), &ni, &mi, rm.data());  // rs.cc:238-322
+  if (rc) return rc;
+  bool fused = k <= kEncMd5MaxK && nfailed <= kMaxRowsPerPass && int64_t(n - 1) * chunk_stride < (int64_t(1) << 32);
+  MulMd5Args a{};
+  if (fused) {
+    for (int j = 0; j < k; j++) a.src_off[j] = static_cast<uint32_t>(inputs[j] * chunk_stride);
+    for (int r = 0; r < nfailed; r++) a.dst_off[r] = static_cast<uint32_t>(failed[r] * chunk_stride);
+    fused = mul_md5_eligible(k, nfailed, len, d_stripes, stripe_stride, a.src_off, d_stripes, stripe_stride, a.dst_off);
+  }
+  if (fused) {
+    if ((rc = ensure_device(ctx->device))) return rc;
+    a.src = d_stripes;
+    a.src_stripe_stride = stripe_stride;
+    a.dst = d_stripes;
+    a.dst_stripe_stride = stripe_stride;
+    a.digests = d_digests;
+    a.digest_stripe_stride = int64_t(nfailed) * 16;
+    a.len = len;
+    a.nstripes = nstripes;
+    a.k = k;
+    a.p = nfailed;
+    a.hash_src = 0;
+    a.hash_dst = 1;
+    for (int r = 0; r < nfailed; r++) a.digest_slot[r] = static_cast<uint8_t>(r);
+    std::memcpy(a.coef, rm.data(), rm.size());
+    return launch_mul_md5(a, ctx->num_cus, pick_stream(ctx, stream));
+  }
+  rc = nxec_rs_recover_stripes(ctx, n, k, failed, nfailed, d_stripes, chunk_stride, stripe_stride, len, nstripes, stream);
+  if (rc) return rc;
+  if ((rc = ensure_device(ctx->device))) return rc;
+  for (int r0 = 0; r0 < nfailed; r0 += kMaxMd5Regions) {  // one MD5 launch per 4 rebuilt chunks
+    Md5Region reg[kMaxMd5Regions];
+    int nr = 0;
+    for (int r = r0; r < nfailed && nr < kMaxMd5Regions; r++, nr++)
+      reg[nr] = Md5Region{d_stripes + failed[r] * chunk_stride, chunk_stride, stripe_stride, len, nstripes,
+                          d_digests + int64_t(r) * 16, int64_t(nfailed) * 16, 1};
+    if ((rc = launch_md5(reg, nr, pick_stream(ctx, stream)))) return rc;
+  }
+  return NXEC_OK;
 }
 
 int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride) {
@@ -748,23 +824,10 @@ int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_obj
   // rs.cc:80), parity chunk (s, i) at d_parity + (s*p + i)*M; with digests
   // wanted, the encode and the MD5 of all n chunks run as one kernel
   const int64_t ds = int64_t(n) * 16;
-  const bool fused = d_md5 && nf > 0 && encode_md5_eligible(k, p, M, d_object, M, k * M, d_parity, M, p * M);
+  MulMd5Args ea;
+  const bool fused = d_md5 && nf > 0 && encode_md5_args(n, k, d_object, M, k * M, d_parity, M, p * M, d_md5, M, nf, ea);
   if (fused) {
-    EncMd5Args ea{};
-    ea.data = d_object;
-    ea.data_chunk_stride = M;
-    ea.data_stripe_stride = k * M;
-    ea.parity = d_parity;
-    ea.parity_chunk_stride = M;
-    ea.parity_stripe_stride = p * M;
-    ea.digests = d_md5;
-    ea.digest_stripe_stride = ds;
-    ea.len = M;
-    ea.nstripes = nf;
-    ea.k = k;
-    ea.p = p;
-    std::memcpy(ea.coef, prow, static_cast<size_t>(p) * k);
-    rc = launch_encode_md5(ea, ctx->num_cus, st);
+    rc = launch_mul_md5(ea, ctx->num_cus, st);
     if (rc) return rc;
   } else if (nf > 0 && p > 0) {
     rc = nxec_stripes_mul(ctx, p, k, prow, d_object, nullptr, M, k * M, d_parity, nullptr, M, p * M, nullptr, M, nf,

@@ -362,6 +362,14 @@ class Context:
                                              stripe_stride, length, nstripes, C.c_void_p(int(digests)), stream),
               "nxec_rs_encode_md5_stripes")
 
+    def rs_recover_md5(self, n: int, k: int, failed: Sequence[int], stripes: int, chunk_stride: int,
+                       stripe_stride: int, length: int, nstripes: int, digests: int, stream=None) -> None:
+        """nxec_rs_recover_md5_stripes: rebuild `failed` in place + MD5 of each rebuilt chunk ([s][nfailed][16])."""
+        f, fp = _i32(failed)
+        check(lib.nxec_rs_recover_md5_stripes(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(stripes)),
+                                              chunk_stride, stripe_stride, length, nstripes, C.c_void_p(int(digests)),
+                                              stream), "nxec_rs_recover_md5_stripes")
+
     def md5_verify_chunks(self, base: int, chunk_stride: int, stripe_stride: int, nchunks: int, length: int,
                           nstripes: int, expected: int, ok: int, nbad=None, stream=None) -> None:
         check(lib.nxec_md5_verify_chunks(C.c_void_p(self.ptr), C.c_void_p(int(base)), chunk_stride, stripe_stride,

@@ -66,6 +66,11 @@ def test_invalid_arguments_rejected_before_device_use():
     rc = _lib.lib.nxec_rs_encode_stripes(None, 3, 4, None, 0, 0, 16, 1, None)
     assert rc == _lib.NXEC_ERR_INVALID
     assert b"invalid" in _lib.lib.nxec_last_error()
+    # the fused checksum entries: no context, bad (n,k), missing buffers, negative sizes
+    f = (ctypes.c_int32 * 1)(0)
+    assert _lib.lib.nxec_rs_encode_md5_stripes(None, 14, 10, None, 0, 0, 256, 1, None, None) == _lib.NXEC_ERR_INVALID
+    assert _lib.lib.nxec_rs_recover_md5_stripes(None, 14, 10, f, 1, None, 0, 0, 256, 1, None, None) == \
+        _lib.NXEC_ERR_INVALID
 
 
 def test_status_forms_return_errors_instead_of_aborting():

@@ -169,3 +169,84 @@ def test_rs_encode_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns):
             assert ga[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
     for x in (a, b, da, db):
         x.free()
+
+
+@pytest.mark.parametrize("n,k,cs,cstride,sstride,ns,failed", [
+    (16, 12, 65536, 65536, 17 * 65536, 40, [0]),           # config-4 geometry, single failure (the repair path)
+    (16, 12, 65536, 65536, 16 * 65536, 21, [15]),          # a parity chunk
+    (14, 10, 4096, 4096 + 16, 14 * (4096 + 16), 300, [1, 4, 11, 13]),  # scattered 4 erasures, padded strides
+    (20, 16, 768, 768, 20 * 768, 33, [0, 1, 2]),
+    (6, 4, 1000, 1008, 6 * 1008, 9, [2]),                  # len not a multiple of 256: recover + MD5 launches
+    (24, 20, 512, 512, 24 * 512, 13, [5, 23]),             # k = 20
+])
+def test_rs_recover_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns, failed):
+    """Repair with checksums (rs.cc:238-322 + Chunk::computeMD5, chunk_manager.cc:1173):
+    the rebuilt chunks equal the oracle's encode of the same data, their digests
+    equal hashlib's, and fused == recover + MD5 launches (NXEC_FUSED_MD5=0)."""
+    data = fill_bytes(ns * k * cs, 313 + cs + len(failed)).reshape(ns, k, cs)
+    full = np.zeros((ns, sstride), dtype=np.uint8)
+    for s in range(ns):
+        st = oracle.rs_encode(n, k, data[s].reshape(-1), cs)
+        for c in range(n):
+            full[s, c * cstride:c * cstride + cs] = st[c]
+    damaged = full.copy()
+    for s in range(ns):
+        for f in failed:
+            damaged[s, f * cstride:f * cstride + cs] = 0xA5
+    outs = []
+    for fused in (True, False):
+        b = nxec.DeviceBuffer(damaged.nbytes)
+        b.upload(damaged)
+        d = nxec.DeviceBuffer(ns * len(failed) * 16)
+        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
+        try:
+            gpu_ctx.rs_recover_md5(n, k, failed, b.ptr, cstride, sstride, cs, ns, d.ptr)
+            gpu_ctx.sync()
+        finally:
+            del os.environ["NXEC_FUSED_MD5"]
+        outs.append((b.download().reshape(ns, sstride), d.download().reshape(ns, len(failed), 16)))
+        b.free()
+        d.free()
+    assert np.array_equal(outs[0][0], full)
+    assert np.array_equal(outs[1][0], full)
+    assert np.array_equal(outs[0][1], outs[1][1])
+    for s in sorted({0, ns // 2, ns - 1}):
+        for r, f in enumerate(failed):
+            assert outs[0][1][s, r].tobytes().hex() == hashlib.md5(full[s, f * cstride:f * cstride + cs].tobytes()).hexdigest()
+
+
+def test_rs_recover_md5_full_batch(gpu_ctx):
+    """Config 4 at full size: 4096 RS(12,4) 1 MiB stripes on the recommended
+    layout (17 MiB stripes), chunk 0 rebuilt with its MD5.  The rebuilt batch's
+    checksum equals the original's; digests equal the two-kernel path's and,
+    for three stripes, hashlib's."""
+    n, k, cs, ns = 16, 12, 1 << 20, 4096
+    cst, sst = nxec.batch_layout(n, cs, 0)
+    buf = nxec.DeviceBuffer(ns * sst)
+    buf.fill_random(4040)
+    gpu_ctx.rs_encode(n, k, buf.ptr, cst, sst, cs, ns)
+    gpu_ctx.sync()
+    ref = buf.checksum()
+    digs = []
+    for fused in (True, False):
+        # erase chunk 0 of every stripe: 0 x chunk 1 -> chunk 0
+        gpu_ctx.stripes_mul(np.zeros((1, 1), dtype=np.uint8), buf.ptr, buf.ptr, src_idx=[1], dst_idx=[0],
+                            src_chunk_stride=cst, src_stripe_stride=sst, dst_chunk_stride=cst, dst_stripe_stride=sst,
+                            length=cs, nstripes=ns)
+        gpu_ctx.sync()
+        assert buf.checksum() != ref
+        d = nxec.DeviceBuffer(ns * 16)
+        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
+        try:
+            gpu_ctx.rs_recover_md5(n, k, [0], buf.ptr, cst, sst, cs, ns, d.ptr)
+            gpu_ctx.sync()
+        finally:
+            del os.environ["NXEC_FUSED_MD5"]
+        assert buf.checksum() == ref
+        digs.append(d.download().reshape(ns, 16))
+        d.free()
+    assert np.array_equal(digs[0], digs[1])
+    for s in (0, 2049, ns - 1):
+        c0 = buf.download(cs, offset=s * sst)
+        assert digs[0][s].tobytes().hex() == hashlib.md5(c0.tobytes()).hexdigest()
+    buf.free()
