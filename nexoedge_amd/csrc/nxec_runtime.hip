@@ -2,6 +2,7 @@
 // points and the drop-in host-buffer encode.  Compute always goes to the
 // gfx950 kernels in nxec_kernels.hip; there is no CPU fallback.
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -28,6 +29,41 @@ namespace nxec {
 
 namespace {
 thread_local std::string g_last_error;
+
+// Copy into pinned staging.  NXEC_NT_STAGING=1 uses streaming (non-temporal)
+// stores: the staging lines are never read by the CPU, so skipping their
+// read-for-ownership halves the DRAM traffic of a large gather
+// (tools/microbench/host_copy.cc measures both on the box).
+bool nt_staging() {
+  static const bool on = [] {
+    const char *e = std::getenv("NXEC_NT_STAGING");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+void stage_copy(void *dst, const void *src, size_t n) {
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const uint8_t *sp = static_cast<const uint8_t *>(src);
+  if (!nt_staging() || n < 4096) {
+    std::memcpy(d, sp, n);
+    return;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+  std::memcpy(d, sp, head);
+  size_t i = head;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 48), e);
+  }
+  _mm_sfence();  // streamed lines visible before the copy engine is told to read them
+  std::memcpy(d + i, sp + i, n - i);
+}
 
 // A host-staging slot: pinned + device buffers and a stream, used by the
 // synchronous host-buffer entry points.  Slots are pooled per context so
@@ -1163,7 +1199,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
       HostPool::get().parallel_for(static_cast<int>(nb) * ni, [&](int item) {  // gather into pinned staging
         const int64_t i = item / ni;
         const int j = item % ni;
-        std::memcpy(b.slot->h + (i * ni + j) * stride, reqs[ids[first + i]].inputs[j], chunk_size);
+        stage_copy(b.slot->h + (i * ni + j) * stride, reqs[ids[first + i]].inputs[j], chunk_size);
       });
       for (int64_t i = 0; i < nb; i++) b.reqs.push_back(ids[first + i]);
       if (agent_trace()) {
@@ -1425,7 +1461,7 @@ int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, in
     const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
     if (p >= 2 && (rc = hip_check(hipEventSynchronize(done[s]), "gather piece sync"))) break;
     frame_copies(fp, first, count, slots[s]->h, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
-      std::memcpy(stage, h_chunks[fp.chunk(item)] + fp.off(item) + o, size_t(nb));
+      stage_copy(stage, h_chunks[fp.chunk(item)] + fp.off(item) + o, size_t(nb));
     });
     hipError_t e = hipSuccess;
     if (fp.segs == 1) {  // whole chunks: one 2D copy scatters the piece to its strided rows
@@ -1879,7 +1915,7 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   uint8_t *hv = inflight.n <= 2 ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
   for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
     const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
-    pool.parallel_for(k, [&](int j) { std::memcpy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
+    pool.parallel_for(k, [&](int j) { stage_copy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
     hipError_t e = hipSuccess;
     uint8_t *base = hv ? hv : slot->d;
     if (!hv) {
