@@ -102,6 +102,14 @@ static void argument_validation() {
         "null ctx");
   CHECK(nxec_rs_encode_stripes(nullptr, 3, 4, buf, 16, 64, 16, 1, nullptr) == NXEC_ERR_INVALID, "n<k");
   CHECK(nxec_md5_chunks(nullptr, buf, 16, 64, 2, 16, 1, buf, nullptr) == NXEC_ERR_INVALID, "md5 null ctx");
+  CHECK(nxec_rs_encode_md5_stripes(nullptr, 14, 10, buf, 256, 14 * 256, 256, 1, buf, nullptr) == NXEC_ERR_INVALID,
+        "encode+md5 null ctx");
+  {
+    const int32_t lost[1] = {0};
+    CHECK(nxec_rs_recover_md5_stripes(nullptr, 14, 10, lost, 1, buf, 256, 14 * 256, 256, 1, buf, nullptr) ==
+              NXEC_ERR_INVALID,
+          "recover+md5 null ctx");
+  }
   CHECK(nxec_agent_encode_batch(nullptr, nullptr, 1, 16, 0) == NXEC_ERR_INVALID, "agent null");
   CHECK(nxec_gather_chunks(nullptr, nullptr, 1, 16, buf, 16, nullptr) == NXEC_ERR_INVALID, "gather null");
   nxec_request_t *req = nullptr;
