@@ -1152,7 +1152,7 @@ static bool agent_trace() {
 // One round of agent requests (validated): grouped by matrix, staged through
 // two double-buffered pinned slots of up to batch_bytes each.
 static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
-                             int64_t batch_bytes, const std::function<void()> &issued = {}) {
+                             int64_t batch_bytes) {
   int rc = ensure_device(ctx->device);
   if (rc) return rc;
   // group requests by (ninputs, noutputs, matrix): one kernel pass per batch of a group
@@ -1228,9 +1228,6 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     if (rc) break;
   }
   if (!rc) rc = agent_d2h(ctx, slots[(cur + kAgentSlots - 1) % kAgentSlots]);  // the last batch's D2H
-  // every batch is queued: the next round may start gathering into its own
-  // slots while this round's last batches drain and scatter
-  if (issued) issued();
   for (int i = 0; i < kAgentSlots; i++) {  // oldest batch first
     AgentBatch &b = slots[(cur + i) % kAgentSlots];
     if (b.slot) {
@@ -1299,17 +1296,11 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       bb = std::max(bb, j->batch_bytes);
     }
     if (round.size() == 1) bb = round[0]->batch_bytes;  // a lone call keeps its own staging bound
-    // leadership passes on as soon as this round's batches are all queued on
-    // the device (rounds then overlap: the next round's host gather and H2D
-    // run while this one's last MD5 chains, D2H and output scatter finish)
-    bool handed = false;
-    auto hand_over = [&] {
-      std::lock_guard<std::mutex> g(ctx->agent_mu);
-      ctx->agent_leader = false;
-      handed = true;
-      ctx->agent_cv.notify_all();
-    };
-    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb, hand_over);
+    // (overlapping rounds -- leadership handed on once a round's batches are
+    // queued -- measured worse: many small rounds, each paying a whole MD5
+    // chain, and two rounds' gathers sharing the host pool; 16 callers 5-11
+    // vs 27-29 GiB/s, profiles/r02_agent_nt_staging.log)
+    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
     const std::string err = rc ? g_last_error : std::string();
     lk.lock();
     for (AgentJob *j : round) {
@@ -1317,7 +1308,7 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       j->error = err;
       j->done = true;
     }
-    if (!handed) ctx->agent_leader = false;  // error before the hand-over
+    ctx->agent_leader = false;
     ctx->agent_cv.notify_all();
   }
   if (job.rc != NXEC_OK) g_last_error = job.error;
