@@ -297,6 +297,22 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream);
 
+/* Read path with checksums: every chunk used as a decode input (the first k
+ * alive ones of each stripe) has its MD5 checked against d_md5 ([ns][n][16],
+ * as nxec_encode_object wrote it) -- Chunk::verifyMD5 on each fetched chunk,
+ * chunk_manager.cc:1548-1556 with verifyChunkChecksum -- and the object is
+ * decoded as nxec_decode_object does, in one pass over the chunks (fused
+ * kernel for the full stripes when k <= 20, the lost data chunks <= 4 and
+ * max_chunk_size is a multiple of 256).  d_ok [ns][n]: byte (s, c) = 1 if
+ * chunk c of stripe s matched, 0 if not; entries of chunks that were not read
+ * are left as they were.  *d_nbad (device, optional, not reset) += mismatches.
+ * A stripe with a mismatch decodes to undefined bytes: re-plan it with the
+ * bad chunks marked failed (the reference fails such a stripe's read). */
+int nxec_decode_object_verify(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                              const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size,
+                              const unsigned char *d_md5, unsigned char *d_object, unsigned char *d_tail,
+                              unsigned char *d_ok, unsigned long long *d_nbad, void *stream);
+
 /* Many objects in one call (the proxy's per-file loop, proxy_file_ops.cc:557-666,
  * over a batch of files): object o (d_objects[o], a HOST array of device
  * pointers, lengths[o] bytes) is split as in nxec_object_layout; its stripes

@@ -64,6 +64,7 @@ _PROTOS = {
     "nxec_md5_chunks": (C.c_int, [vp, vp, i64, i64, C.c_int, i64, i64, vp, vp]),
     "nxec_rs_encode_md5_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, i64, vp, vp]),
     "nxec_rs_recover_md5_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, i64, vp, vp]),
+    "nxec_decode_object_verify": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp, vp, vp, vp]),
     "nxec_md5_verify_chunks": (C.c_int, [vp, vp, i64, i64, C.c_int, i64, i64, vp, vp, vp, vp]),
     "nxec_object_layout": (C.c_int, [C.c_int, C.c_int, i64, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, vp, vp]),

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
         }
         if (PROBE & 2) {
           if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
-        } else {
+        } else if (a.p > 0) {  // wave-uniform (p = 0: a verified copy, no rows to compute)
           lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
         }
         // materialise the accumulators per source pair: left alone, LLVM
@@ -180,6 +180,11 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
       uint32_t o[4][4];
       rows_of(acc, o);
       const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+      if (a.any_copy) {  // full-output decode: surviving data chunks pass through
+#pragma unroll
+        for (int j = 0; j < K; j++)
+          if (a.copy_off[j] != kNoCopy) st_stream(dst + a.copy_off[j] + off, d[j]);
+      }
 #pragma unroll
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
@@ -284,8 +289,16 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
     md5_pad_aligned(st, static_cast<uint64_t>(a.len));
     const int ls = h / nh, c = h - ls * nh;
     uint8_t *out = a.digests + (s0 + ls) * a.digest_stripe_stride + a.digest_slot[c] * 16;
+    if (a.ok) {  // Chunk::verifyMD5 (chunk_manager.cc:1553-1555): compare with the stored digest
+      bool same = true;
 #pragma unroll
-    for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+      for (int i = 0; i < 16; i++) same &= out[i] == static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));
+      a.ok[(s0 + ls) * a.ok_stripe_stride + a.digest_slot[c]] = same ? 1 : 0;
+      if (!same && a.nbad) atomicAdd(a.nbad, 1ull);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+    }
   }
 }
 
@@ -301,8 +314,8 @@ const EmKernel kEmProbe[4] = {&k_mul_md5<10, 0>, &k_mul_md5<10, 1>, &k_mul_md5<1
 }  // namespace
 
 bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src_stripe_stride, const uint32_t *src_off,
-                     const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off) {
-  if (k < 1 || k > kEncMd5MaxK || rows < 1 || rows > kMaxRowsPerPass) return false;
+                      const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off, const uint32_t *copy_off) {
+  if (k < 1 || k > kEncMd5MaxK || rows < 0 || rows > kMaxRowsPerPass) return false;
   if (len <= 0 || len % kEncMd5Step != 0 || len / kEncMd5Step >= (int64_t(1) << 31)) return false;
   if (const char *e = std::getenv("NXEC_FUSED_MD5"))
     if (e[0] == '0') return false;  // A/B: two kernels (coding, then MD5)
@@ -310,6 +323,9 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
                   static_cast<uint64_t>(src_stripe_stride) | static_cast<uint64_t>(dst_stripe_stride);
   for (int j = 0; j < k; j++) bits |= src_off[j];
   for (int r = 0; r < rows; r++) bits |= dst_off[r];
+  if (copy_off)
+    for (int j = 0; j < k; j++)
+      if (copy_off[j] != kNoCopy) bits |= copy_off[j];
   return (bits & 15) == 0;
 }
 

@@ -92,11 +92,12 @@ struct Md5Region {
   uint8_t *digests;
   int64_t dig_stripe_stride;
   int nchunks;
+  // verify mode (ok != nullptr): `digests` holds the expected digests; chunk
+  // (s, i) writes ok[s*ok_stripe_stride + i] = match, *nbad += mismatches
+  uint8_t *ok = nullptr;
+  int64_t ok_stripe_stride = 0;
 };
-// verify mode (ok != nullptr, one region): `digests` holds the expected
-// digests; ok[s*nchunks + i] = match, *nbad += mismatches (nbad optional)
-int launch_md5(const Md5Region *regions, int nregions, void *stream, uint8_t *ok = nullptr,
-               unsigned long long *nbad = nullptr);
+int launch_md5(const Md5Region *regions, int nregions, void *stream, unsigned long long *nbad = nullptr);
 int launch_checksum(const void *d, size_t bytes, uint64_t *d_out, void *stream);
 
 // Variable-length batch (many objects per call): stripe s has its own chunk
@@ -169,13 +170,24 @@ struct MulMd5Args {
   int32_t hash_prio;             // hash waves at s_setprio 1 (set by launch_mul_md5)
   uint32_t src_off[NXEC_MAX_K + 1];
   uint32_t dst_off[kMaxRowsPerPass];
+  // pass-through (full-output decode): source j also stored to dst +
+  // s*dst_stripe_stride + copy_off[j] unless kNoCopy
+  int32_t any_copy;
+  uint32_t copy_off[NXEC_MAX_K + 1];
   uint8_t digest_slot[NXEC_MAX_K + 1 + kMaxRowsPerPass];
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
+  // verify mode (ok != nullptr): `digests` holds the expected digests; hashed
+  // chunk i of stripe s writes ok[s*ok_stripe_stride + digest_slot[i]] = match
+  // and counts a mismatch into *nbad (optional)
+  uint8_t *ok;
+  int64_t ok_stripe_stride;
+  unsigned long long *nbad;
 };
-// k <= kEncMd5MaxK, 1 <= rows <= 4, len a positive multiple of kEncMd5Step,
+// k <= kEncMd5MaxK, 0 <= rows <= 4, len a positive multiple of kEncMd5Step,
 // 16-byte aligned buffers, strides and offsets (NXEC_FUSED_MD5=0 disables, for A/B)
 bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src_stripe_stride, const uint32_t *src_off,
-                      const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off);
+                      const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off,
+                      const uint32_t *copy_off = nullptr);
 int prepare_encode_md5();
 int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 

@@ -166,9 +166,9 @@ struct Md5Args {
   int nregions;
   const Md5Item *items;  // list mode (items != nullptr): lane c hashes items[c]
   int64_t nitems;
-  // verify mode (ok != nullptr): the region's digests are the expected ones,
-  // lane c writes ok[c] = digest matches, and counts mismatches into *nbad
-  uint8_t *ok;
+  // verify mode (a region's ok != nullptr): its digests are the expected
+  // ones; chunk (s, i) writes ok[s*ok_stripe_stride + i] = digest matches and
+  // counts a mismatch into *nbad
   unsigned long long *nbad;
 };
 
@@ -179,6 +179,7 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
   const uint8_t *p;
   int64_t len;
   uint8_t *out;
+  uint8_t *ok = nullptr;  // verify mode: this chunk's ok flag
   if (args.items) {
     if (c >= args.nitems) return;
     const Md5Item it = args.items[c];
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
     p = rg.base + s * rg.stripe_stride + ci * rg.chunk_stride;
     len = rg.len;
     out = rg.digests + s * rg.dig_stripe_stride + ci * 16;
+    if (rg.ok) ok = rg.ok + s * rg.ok_stripe_stride + ci;
   }
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 15) == 0;
   uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
@@ -244,11 +246,11 @@ __global__ __launch_bounds__(64) void k_md5(const Md5Args args) {
     }
     md5_block(h, m);
   }
-  if (args.ok) {  // Chunk::verifyMD5: recompute and compare (chunk_manager.cc:1555, container_manager.cc:187-207)
+  if (ok) {  // Chunk::verifyMD5: recompute and compare (chunk_manager.cc:1555, container_manager.cc:187-207)
     bool same = true;
 #pragma unroll
     for (int i = 0; i < 16; i++) same &= out[i] == static_cast<uint8_t>(h[i / 4] >> (8 * (i % 4)));
-    args.ok[c] = same ? 1 : 0;
+    *ok = same ? 1 : 0;
     if (!same && args.nbad) atomicAdd(args.nbad, 1ull);
     return;
   }
@@ -285,9 +287,8 @@ Md5Kernel md5_kernel() {
 
 }  // namespace
 
-int launch_md5(const Md5Region *regions, int nregions, void *stream, uint8_t *ok, unsigned long long *nbad) {
+int launch_md5(const Md5Region *regions, int nregions, void *stream, unsigned long long *nbad) {
   Md5Args args{};
-  args.ok = ok;
   args.nbad = nbad;
   int64_t total = 0;
   int nr = 0;

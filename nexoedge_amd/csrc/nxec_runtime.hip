@@ -691,8 +691,8 @@ int nxec_md5_verify_chunks(nxec_ctx_t *ctx, const unsigned char *d_base, int64_t
   if (rc) return rc;
   // the kernel only reads the digests in verify mode
   const Md5Region r{d_base, chunk_stride, stripe_stride, len, nstripes, const_cast<unsigned char *>(d_expected),
-                    int64_t(nchunks) * 16, nchunks};
-  return launch_md5(&r, 1, pick_stream(ctx, stream), d_ok, d_nbad);
+                    int64_t(nchunks) * 16, nchunks, d_ok, nchunks};
+  return launch_md5(&r, 1, pick_stream(ctx, stream), d_nbad);
 }
 
 }  // extern "C"
@@ -1086,6 +1086,96 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
   rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks + nf * n * M, M, n * M, d_tail, cs_last,
                               k * cs_last, cs_last, 1, st);
   if (rc) return rc;
+  const int64_t rem = length - nf * k * M;
+  return hip_check(hipMemcpyAsync(d_object + nf * k * M, d_tail, rem, hipMemcpyDeviceToDevice, st), "tail copy");
+}
+
+int nxec_decode_object_verify(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                              const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size,
+                              const unsigned char *d_md5, unsigned char *d_object, unsigned char *d_tail,
+                              unsigned char *d_ok, unsigned long long *d_nbad, void *stream) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  int64_t ns = 0, nf = 0, cs_last = 0;
+  int rc = nxec_object_layout(n, k, length, max_chunk_size, &ns, &nf, &cs_last);
+  if (rc) return rc;
+  if (ns == 0) return NXEC_OK;
+  const int64_t M = max_chunk_size;
+  const bool tail = ns > nf;
+  if (!d_chunks || !d_object || !d_md5 || !d_ok || (tail && !d_tail))
+    return set_error(NXEC_ERR_INVALID, "nxec_decode_object_verify: null buffer");
+  std::vector<int32_t> inputs(n);
+  int ni = 0, mi = 0;
+  if ((rc = nxec_rs_plan(n, k, failed, nfailed, 0, inputs.data(), &ni, &mi, nullptr))) return rc;  // rs.cc:252-265
+  if ((rc = ensure_device(ctx->device))) return rc;
+  hipStream_t st = pick_stream(ctx, stream);
+  std::vector<int32_t> targets;
+  for (int i = 0; i < nfailed; i++)
+    if (failed[i] < k) targets.push_back(failed[i]);
+  const int e = static_cast<int>(targets.size());
+  // verify the k inputs of `nst` stripes of `len`-byte chunks (MD5 launches, 4 chunks each)
+  auto verify = [&](const unsigned char *chunks, int64_t len, int64_t nst, int64_t s0) -> int {
+    for (int j0 = 0; j0 < k; j0 += kMaxMd5Regions) {
+      Md5Region reg[kMaxMd5Regions];
+      int nr = 0;
+      for (int j = j0; j < k && nr < kMaxMd5Regions; j++, nr++) {
+        const int id = inputs[j];
+        reg[nr] = Md5Region{chunks + id * M, M, n * M, len, nst,
+                            const_cast<unsigned char *>(d_md5) + (s0 * n + id) * 16, int64_t(n) * 16, 1,
+                            d_ok + s0 * n + id, n};
+      }
+      if (int r = launch_md5(reg, nr, st, d_nbad)) return r;
+    }
+    return NXEC_OK;
+  };
+  if (nf > 0) {
+    MulMd5Args a{};
+    bool fused = e <= kMaxRowsPerPass && k <= kEncMd5MaxK && int64_t(n - 1) * M < (int64_t(1) << 32) &&
+                 int64_t(k) * M < (int64_t(1) << 32);
+    if (fused) {
+      a.any_copy = 0;
+      for (int j = 0; j < k; j++) {
+        a.src_off[j] = static_cast<uint32_t>(inputs[j] * M);
+        a.copy_off[j] = inputs[j] < k ? static_cast<uint32_t>(inputs[j] * M) : kNoCopy;
+        a.any_copy |= inputs[j] < k;
+        a.digest_slot[j] = static_cast<uint8_t>(inputs[j]);
+      }
+      for (int r = 0; r < e; r++) a.dst_off[r] = static_cast<uint32_t>(targets[r] * M);
+      fused = mul_md5_eligible(k, e, M, d_chunks, n * M, a.src_off, d_object, k * M, a.dst_off, a.copy_off);
+    }
+    if (fused) {
+      if (e > 0) {
+        std::vector<uint8_t> m(static_cast<size_t>(e) * k);
+        if ((rc = nxec_rs_decode_matrix(n, k, inputs.data(), targets.data(), e, m.data()))) return rc;  // rs.cc:196,228
+        std::memcpy(a.coef, m.data(), m.size());
+      }
+      a.src = d_chunks;
+      a.src_stripe_stride = n * M;
+      a.dst = d_object;
+      a.dst_stripe_stride = k * M;
+      a.digests = const_cast<unsigned char *>(d_md5);
+      a.digest_stripe_stride = int64_t(n) * 16;
+      a.ok = d_ok;
+      a.ok_stripe_stride = n;
+      a.nbad = d_nbad;
+      a.len = M;
+      a.nstripes = nf;
+      a.k = k;
+      a.p = e;
+      a.hash_src = 1;
+      a.hash_dst = 0;
+      if ((rc = launch_mul_md5(a, ctx->num_cus, st))) return rc;
+    } else {
+      if ((rc = verify(d_chunks, M, nf, 0))) return rc;
+      if ((rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks, M, n * M, d_object, M, k * M, M, nf, st)))
+        return rc;
+    }
+  }
+  if (!tail) return NXEC_OK;
+  // last stripe (chunks of cs_last bytes in the same slots): verify, decode to scratch, keep the unpadded bytes
+  if ((rc = verify(d_chunks + nf * n * M, cs_last, 1, nf))) return rc;
+  if ((rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks + nf * n * M, M, n * M, d_tail, cs_last,
+                                   k * cs_last, cs_last, 1, st)))
+    return rc;
   const int64_t rem = length - nf * k * M;
   return hip_check(hipMemcpyAsync(d_object + nf * k * M, d_tail, rem, hipMemcpyDeviceToDevice, st), "tail copy");
 }

@@ -403,6 +403,16 @@ class Context:
                                      max_chunk_size, C.c_void_p(int(obj)), C.c_void_p(int(tail) if tail else None),
                                      stream), "nxec_decode_object")
 
+    def decode_object_verify(self, n: int, k: int, failed: Sequence[int], chunks: int, length: int,
+                             max_chunk_size: int, md5: int, obj: int, tail, ok: int, nbad=None, stream=None) -> None:
+        """nxec_decode_object_verify: decode_object + MD5 check of every chunk read (ok [ns][n] bytes)."""
+        f, fp = _i32(failed)
+        check(lib.nxec_decode_object_verify(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(chunks)),
+                                            length, max_chunk_size, C.c_void_p(int(md5)), C.c_void_p(int(obj)),
+                                            C.c_void_p(int(tail) if tail else None), C.c_void_p(int(ok)),
+                                            C.c_void_p(int(nbad) if nbad else None), stream),
+              "nxec_decode_object_verify")
+
     def agent_encode_batch(self, reqs, chunk_size: int, batch_bytes: int = 0) -> None:
         """nxec_agent_encode_batch: reqs = [(matrix (no x ni), inputs [ni arrays], outputs [no arrays],
         md5 (no x 16 uint8 array) or None)], host numpy buffers of chunk_size bytes."""

@@ -250,3 +250,69 @@ def test_rs_recover_md5_full_batch(gpu_ctx):
         c0 = buf.download(cs, offset=s * sst)
         assert digs[0][s].tobytes().hex() == hashlib.md5(c0.tobytes()).hexdigest()
     buf.free()
+
+
+def _object_chunks(n, k, M, obj, par_h, length):
+    """[ns][n][M] chunks as the agents store them: data chunks cut from the
+    object (last stripe zero padded, chunk_manager.cc:390-399), parity from
+    nxec_encode_object's [ns][n-k][M] parity."""
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    ch = np.zeros((ns, n, M), dtype=np.uint8)
+    for s in range(ns):
+        cs = M if s < nf else cl
+        sd = np.zeros(k * cs, dtype=np.uint8)
+        piece = obj[s * k * M:s * k * M + k * cs]
+        sd[:len(piece)] = piece
+        ch[s, :k, :cs] = sd.reshape(k, cs)
+        ch[s, k:, :cs] = par_h[s, :, :cs]
+    return ch
+
+
+@pytest.mark.parametrize("failed", [[], [1, 4, 11, 13], [10, 11], [0, 1, 2, 3]])
+@pytest.mark.parametrize("fused", [True, False])
+def test_decode_object_verify(gpu_ctx, failed, fused):
+    """Read path with checksums (Chunk::verifyMD5 of every fetched chunk,
+    chunk_manager.cc:1548-1556, then decodeFile): the object comes back intact,
+    every chunk read is flagged ok, a corrupted input is flagged and counted."""
+    n, k, M = 14, 10, 65536
+    length = 5 * k * M + 77777
+    obj = fill_bytes(length, 6060 + len(failed))
+    ob = nxec.DeviceBuffer(length)
+    ob.upload(obj)
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    par = nxec.DeviceBuffer(ns * (n - k) * M)
+    tail = nxec.DeviceBuffer(k * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, tail.ptr, md5.ptr)
+    gpu_ctx.sync()
+    ch = _object_chunks(n, k, M, obj, par.download().reshape(ns, n - k, M), length)
+    alive = [c for c in range(n) if c not in failed][:k]
+    bad_s, bad_c = 2, alive[0]
+    ch[bad_s, bad_c, 100] ^= 0x5A  # one fetched chunk corrupted in transit
+    for c in failed:
+        ch[:, c] = 0xEE
+    cb = nxec.DeviceBuffer(ch.nbytes)
+    cb.upload(ch)
+    out = nxec.DeviceBuffer(length)
+    ok = nxec.DeviceBuffer(ns * n)
+    ok.memset(7)
+    nb = nxec.DeviceBuffer(8)
+    nb.memset(0)
+    os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
+    try:
+        gpu_ctx.decode_object_verify(n, k, failed, cb.ptr, length, M, md5.ptr, out.ptr, tail.ptr, ok.ptr, nb.ptr)
+        gpu_ctx.sync()
+    finally:
+        del os.environ["NXEC_FUSED_MD5"]
+    flags = ok.download().reshape(ns, n)
+    want = np.full((ns, n), 7, dtype=np.uint8)
+    want[:, alive] = 1
+    want[bad_s, bad_c] = 0
+    assert np.array_equal(flags, want)
+    assert int(nb.download().view(np.uint64)[0]) == 1
+    got = out.download()
+    keep = np.ones(length, dtype=bool)
+    keep[bad_s * k * M:(bad_s + 1) * k * M] = False  # the flagged stripe is re-planned by the caller
+    assert np.array_equal(got[keep], obj[keep])
+    for b in (ob, par, tail, md5, cb, out, ok, nb):
+        b.free()
