@@ -351,7 +351,7 @@ def wl_write14(args, ctx, stream, rank):
               "byte_accounting": "n*cs per stripe: one HBM pass (k*cs read, (n-k)*cs written); the MD5 of all n "
                                  "chunks reads the same bytes from LDS"}
     return Workload("write14", "GiB/s RS(10,4) encode + per-chunk MD5, 1 MiB chunks, device-resident", config, ops,
-                    [buf, dig], f"k_encode_md5<K={k}> (fused encode + MD5; MD5-chain-bound, not HBM-bound)", ns)
+                    [buf, dig], f"k_mul_md5<K={k}> (fused encode + MD5; MD5-chain-bound, not HBM-bound)", ns)
 
 
 def wl_object(args, ctx, stream, rank):
@@ -372,19 +372,27 @@ def wl_object(args, ctx, stream, rank):
     ctx.rs_encode(n, k, chunks.ptr, M, n * M, M, ns, stream)
     out = nxec.DeviceBuffer(length)
     failed = list(range(min(4, p)))
+    cmd5 = nxec.DeviceBuffer(ns * n * 16)  # digests of the stored chunks, for the verified read
+    ctx.md5_chunks(chunks.ptr, M, n * M, n, M, ns, cmd5.ptr, stream)
+    ok = nxec.DeviceBuffer(ns * n)
     ops = [
         ("write_encode_object_md5", lambda i: ctx.encode_object(n, k, obj.ptr, length, M, par.ptr, None, md5.ptr, stream),
          ns * n * M),
         ("read_decode_object", lambda i: ctx.decode_object(n, k, failed, chunks.ptr, length, M, out.ptr, None, stream),
          2 * ns * k * M),
+        ("read_verify_decode_object",
+         lambda i: ctx.decode_object_verify(n, k, failed, chunks.ptr, length, M, cmd5.ptr, out.ptr, None, ok.ptr,
+                                            None, stream),
+         2 * ns * k * M),
     ]
     config = {"workload": f"object of {ns} RS({n},{k}) stripes ({length >> 30} GiB), {M >> 10} KiB chunks: write = "
-                          f"encode_object + MD5 of all chunks, read = decode_object with chunks {failed} lost",
+                          f"encode_object + MD5 of all chunks, read = decode_object with chunks {failed} lost, "
+                          "then the same read with every input chunk's MD5 verified (decode_object_verify)",
               "stripes_per_gpu": ns, "chunk_bytes": M,
               "byte_accounting": "write: n*cs per stripe (one fused encode + MD5 pass); read: full-output decode "
                                  "2k*cs per stripe"}
     return Workload("object", "GiB/s object write (encode+MD5) + read (decode), RS(10,4), 1 MiB chunks, device-resident",
-                    config, ops, [obj, par, md5, chunks, out], "encode_object (fused k_encode_md5)", ns)
+                    config, ops, [obj, par, md5, chunks, out, cmd5, ok], "encode_object (fused k_mul_md5)", ns)
 
 
 def wl_files(args, ctx, stream, rank):

@@ -49,12 +49,10 @@ namespace nxec {
 namespace {
 
 using dev::build_tables;
-using dev::ld_stream;
 using dev::md5_block;
 using dev::md5_init;
 using dev::md5_pad_aligned;
 using dev::rows_of;
-using dev::st_stream;
 using dev::u32x4;
 
 constexpr int kEmBlock = 512;                  // 4 code waves + 4 hash waves
@@ -115,6 +113,19 @@ constexpr int em_depth() {
   return K * 4 * 4 <= 170 ? 4 : K * 4 * 3 <= 170 ? 3 : 2;
 }
 
+// Raw buffer resource over [base, base + 4 GiB) (gfx9 descriptor word 3) and
+// nontemporal 16-byte accesses through it (cache policy 2 = nt on gfx950).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t em_rsrc(const void *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ u32x4 em_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2));
+}
+__device__ __forceinline__ void em_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)), v),
+                                         r, voff, soff, 2);
+}
+
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
@@ -124,11 +135,15 @@ __device__ __forceinline__ void lds_barrier() {
 // PROBE (design probes only, K = 10, NXEC_EM_PROBE; outputs are NOT valid):
 // bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
 // the table lookups (parity = first source), to time each role alone.
-template <int K, int PROBE = 0>
+// HSRC: the sources are hashed too (write and verified-read paths) -- a
+// template parameter, not a runtime flag: a wave-uniform branch around the
+// sources' LDS writes kept every ring buffer live longer and spilled from
+// k = 8 (180 instead of 256+ VGPRs at k = 10).
+template <int K, bool HSRC, int PROBE = 0>
 __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = a.nhashed;  // hashed chunks per stripe: LDS rows per stripe
-  const int hsrc = a.hash_src ? K : 0;  // rows before the outputs' rows
+  constexpr int hsrc = HSRC ? K : 0;  // rows before the outputs' rows
   const int S = a.stripes_per_group;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
@@ -147,13 +162,20 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
     // and waits only for the ring slot it consumes.
     const int item = threadIdx.x;
     const int ls = item < nS * kEmVecs ? item / kEmVecs : 0, v = item % kEmVecs;
-    const uint8_t *src = a.src + (s0 + ls) * a.src_stripe_stride + v * 16;
-    uint8_t *dst = a.dst + (s0 + ls) * a.dst_stripe_stride + v * 16;
+    // Global accesses go through buffer resources based at the group's first
+    // stripe: the lane's part of the address is one 32-bit VGPR, the chunk
+    // and step part an SGPR offset -- no 64-bit address pair per source,
+    // output and copy (those pushed the copy-through variant into spills).
+    // launch_mul_md5 checks that every offset of a group fits in 32 bits.
+    const __amdgpu_buffer_rsrc_t rsrc_src = em_rsrc(a.src + s0 * a.src_stripe_stride);
+    const __amdgpu_buffer_rsrc_t rsrc_dst = em_rsrc(a.dst + s0 * a.dst_stripe_stride);
+    const uint32_t vsrc = static_cast<uint32_t>(ls * a.src_stripe_stride) + v * 16;
+    const uint32_t vdst = static_cast<uint32_t>(ls * a.dst_stripe_stride) + v * 16;
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
     auto load = [&](int step, u32x4(&d)[K]) {
-      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+      const uint32_t off = static_cast<uint32_t>(step) * kEncMd5Step;
 #pragma unroll
-      for (int j = 0; j < K; j++) d[j] = ld_stream(src + a.src_off[j] + off);
+      for (int j = 0; j < K; j++) d[j] = em_load(rsrc_src, vsrc, a.src_off[j] + off);
     };
     auto run = [&](int step, const u32x4(&d)[K]) {
       uint8_t *rb = row + (step & 1) * buf_bytes;
@@ -165,6 +187,11 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
         if (hsrc) {  // wave-uniform
           *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
           if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
+        }
+        if (a.any_copy) {  // full-output decode: surviving data chunks pass through
+          const uint32_t off = static_cast<uint32_t>(step) * kEncMd5Step;
+          if (a.copy_off[j] != kNoCopy) em_store(rsrc_dst, vdst, a.copy_off[j] + off, d[j]);
+          if (j + 1 < K && a.copy_off[j + 1] != kNoCopy) em_store(rsrc_dst, vdst, a.copy_off[j + 1] + off, d[j + 1]);
         }
         if (PROBE & 2) {
           if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
@@ -179,17 +206,12 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
       }
       uint32_t o[4][4];
       rows_of(acc, o);
-      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
-      if (a.any_copy) {  // full-output decode: surviving data chunks pass through
-#pragma unroll
-        for (int j = 0; j < K; j++)
-          if (a.copy_off[j] != kNoCopy) st_stream(dst + a.copy_off[j] + off, d[j]);
-      }
+      const uint32_t off = static_cast<uint32_t>(step) * kEncMd5Step;
 #pragma unroll
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          st_stream(dst + a.dst_off[r] + off, pv);
+          em_store(rsrc_dst, vdst, a.dst_off[r] + off, pv);
           if (a.hash_dst) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;
         }
       }
@@ -303,13 +325,16 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
 }
 
 using EmKernel = void (*)(const MulMd5Args);
-template <int... Ks>
+template <bool HSRC, int... Ks>
 constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int, Ks...>) {
-  return {{&k_mul_md5<Ks + 1>...}};
+  return {{&k_mul_md5<Ks + 1, HSRC>...}};
 }
-const std::array<EmKernel, kEncMd5MaxK> kEm = em_table(std::make_integer_sequence<int, kEncMd5MaxK>{});
+// [hash_src][k - 1]
+const std::array<EmKernel, kEncMd5MaxK> kEm[2] = {em_table<false>(std::make_integer_sequence<int, kEncMd5MaxK>{}),
+                                                  em_table<true>(std::make_integer_sequence<int, kEncMd5MaxK>{})};
 
-const EmKernel kEmProbe[4] = {&k_mul_md5<10, 0>, &k_mul_md5<10, 1>, &k_mul_md5<10, 2>, &k_mul_md5<10, 3>};
+const EmKernel kEmProbe[4] = {&k_mul_md5<10, true, 0>, &k_mul_md5<10, true, 1>, &k_mul_md5<10, true, 2>,
+                              &k_mul_md5<10, true, 3>};
 
 }  // namespace
 
@@ -330,11 +355,12 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
 }
 
 int prepare_encode_md5() {
-  for (int k = 1; k <= kEncMd5MaxK; k++) {
+  for (int i = 0; i < 2 * kEncMd5MaxK; i++) {
+    const EmKernel fn = kEm[i / kEncMd5MaxK][i % kEncMd5MaxK];
     hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kEm[k - 1])) != hipSuccess || fa.sharedSizeBytes != 0)
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
       return set_error(NXEC_ERR_HIP, "k_mul_md5: static LDS present (the tables must start at LDS byte 0)");
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEm[k - 1]),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5): %s", hipGetErrorString(e));
   }
@@ -363,9 +389,9 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   const int64_t grid = (a.nstripes + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
   const int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
-  EmKernel fn = kEm[a.k - 1];
+  EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
   if (const char *e = std::getenv("NXEC_EM_PROBE"))
-    if (a.k == 10) fn = kEmProbe[std::atoi(e) & 3];
+    if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 3];
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();

@@ -63,3 +63,33 @@ if len(args) != 4:
     buf.free()
     dig.free()
     ctx.close()
+
+# read with checksums: decode_object_verify of a 4096 x RS(10,4) 1 MiB object, 4 data chunks lost
+if len(args) != 4:
+    ctx = nxec.Context(0)
+    n, k, M, ns = 14, 10, 1 << 20, 4096
+    length = ns * k * M
+    chunks = nxec.DeviceBuffer(ns * n * M)
+    chunks.fill_random(21)
+    ctx.rs_encode(n, k, chunks.ptr, M, n * M, M, ns)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    ctx.md5_chunks(chunks.ptr, M, n * M, n, M, ns, md5.ptr)
+    out = nxec.DeviceBuffer(length)
+    ok = nxec.DeviceBuffer(ns * n)
+    failed = [0, 1, 2, 3]
+    alg = ns * 2 * k * M  # read k survivors, write k data chunks (full-output decode), as bench --workload object
+    for mode in ("1", "0", "1", "0"):
+        os.environ["NXEC_FUSED_MD5"] = mode
+        ctx.decode_object_verify(n, k, failed, chunks.ptr, length, M, md5.ptr, out.ptr, None, ok.ptr)
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(6):
+            ctx.decode_object_verify(n, k, failed, chunks.ptr, length, M, md5.ptr, out.ptr, None, ok.ptr)
+        ctx.sync()
+        ms = (time.perf_counter() - t0) / 6 * 1e3
+        print(f"RS(14,10) read + verify, 4 data chunks lost, 1 MiB x {ns}: {'fused' if mode == '1' else 'two  '} "
+              f"{ms:8.3f} ms ({alg / ms / 1e6 / 8000:.3f} of 8 TB/s of 2k*cs)", flush=True)
+    assert (ok.download().reshape(ns, n)[:, 4:] == 1).all()
+    for b in (chunks, md5, out, ok):
+        b.free()
+    ctx.close()
