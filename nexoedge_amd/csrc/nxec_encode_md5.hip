@@ -107,10 +107,11 @@ __device__ __forceinline__ void lookup_pair(int j0, bool two, const u32x4 d0, co
   }
 }
 
-// prefetch ring depth: as many 4K-VGPR source buffers as fit in ~170 VGPRs
+// prefetch ring depth: as many 4K-VGPR source buffers as fit in ~200 VGPRs
+// (the rest of the code role needs ~20 with buffer-resource addressing)
 template <int K>
 constexpr int em_depth() {
-  return K * 4 * 4 <= 170 ? 4 : K * 4 * 3 <= 170 ? 3 : 2;
+  return K * 4 * 4 <= 200 ? 4 : K * 4 * 3 <= 200 ? 3 : 2;
 }
 
 // Raw buffer resource over [base, base + 4 GiB) (gfx9 descriptor word 3) and
@@ -383,6 +384,8 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   int64_t S = std::min(kEmMaxStripes, kEmMaxRows / n);  // n: hashed chunks per stripe
   const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
   if (per_cu < S) S = per_cu;
+  if (const char *e = std::getenv("NXEC_EM_S"))  // tuning only: stripes per workgroup
+    S = std::max<int64_t>(1, std::min<int64_t>(std::atoi(e), std::min(kEmMaxStripes, kEmMaxRows / n)));
   a.stripes_per_group = static_cast<int32_t>(S);
   a.hash_prio = 0;
   if (const char *e = std::getenv("NXEC_EM_PRIO")) a.hash_prio = std::atoi(e);
