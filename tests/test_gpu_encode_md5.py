@@ -316,3 +316,42 @@ def test_decode_object_verify(gpu_ctx, failed, fused):
     assert np.array_equal(got[keep], obj[keep])
     for b in (ob, par, tail, md5, cb, out, ok, nb):
         b.free()
+
+
+def test_decode_object_verify_many_losses(gpu_ctx):
+    """More lost data chunks than one fused pass rebuilds (e = 5 > 4): the
+    verify launches + decode path, same contract."""
+    n, k, M = 20, 14, 4096
+    length = 7 * k * M + 999
+    failed = [0, 2, 4, 6, 8]
+    obj = fill_bytes(length, 8181)
+    ob = nxec.DeviceBuffer(length)
+    ob.upload(obj)
+    ns, nf, cl = nxec.object_layout(n, k, length, M)
+    par = nxec.DeviceBuffer(ns * (n - k) * M)
+    tail = nxec.DeviceBuffer(k * M)
+    md5 = nxec.DeviceBuffer(ns * n * 16)
+    gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, tail.ptr, md5.ptr)
+    gpu_ctx.sync()
+    ch = _object_chunks(n, k, M, obj, par.download().reshape(ns, n - k, M), length)
+    alive = [c for c in range(n) if c not in failed][:k]
+    ch[ns - 1, alive[-1], 3] ^= 1  # corrupt an input of the (ragged) last stripe
+    for c in failed:
+        ch[:, c] = 0
+    cb = nxec.DeviceBuffer(ch.nbytes)
+    cb.upload(ch)
+    out = nxec.DeviceBuffer(length)
+    ok = nxec.DeviceBuffer(ns * n)
+    ok.memset(9)
+    nb = nxec.DeviceBuffer(8)
+    nb.memset(0)
+    gpu_ctx.decode_object_verify(n, k, failed, cb.ptr, length, M, md5.ptr, out.ptr, tail.ptr, ok.ptr, nb.ptr)
+    gpu_ctx.sync()
+    want = np.full((ns, n), 9, dtype=np.uint8)
+    want[:, alive] = 1
+    want[ns - 1, alive[-1]] = 0
+    assert np.array_equal(ok.download().reshape(ns, n), want)
+    assert int(nb.download().view(np.uint64)[0]) == 1
+    assert np.array_equal(out.download()[:nf * k * M], obj[:nf * k * M])
+    for b in (ob, par, tail, md5, cb, out, ok, nb):
+        b.free()
