@@ -133,6 +133,67 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Hash waves of the fused kernels: lane h owns LDS row h (kEncMd5Step bytes
+// of its chunk per step, two step buffers buf_bytes apart).  The row of step s
+// is read right after barrier s, while the lane hashes step s - 1 from
+// registers: the reads (queued behind the code waves' lookups in the LDS) get
+// a whole step to land.  They are complete before barrier s + 1 (its fence
+// waits for them), so the code waves may refill that buffer afterwards.
+// Every hash wave takes part in every barrier; st is the state after the
+// last data block (not yet padded).  PROBE bit 0: XOR instead of MD5 rounds.
+template <int PROBE>
+__device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes, int h, bool active, int nsteps,
+                                          uint32_t (&st)[4]) {
+  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
+  md5_init(st);
+  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
+    const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
+#pragma unroll
+    for (int i = 0; i < kEmVecs; i++) {
+      const u32x4 x = p[i];
+      m[4 * i] = x.x;
+      m[4 * i + 1] = x.y;
+      m[4 * i + 2] = x.z;
+      m[4 * i + 3] = x.w;
+    }
+  };
+  auto hash = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
+    if (PROBE & 1) {
+#pragma unroll
+      for (int i = 0; i < kEncMd5Step / 4; i++) st[i & 3] ^= m[i];
+    } else {
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+    }
+  };
+  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
+  lds_barrier();
+  if (active) fetch(0, m0);
+  int step = 1;
+  for (; step + 2 <= nsteps; step += 2) {
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+    }
+    lds_barrier();
+    if (active) {
+      fetch(step + 1, m0);
+      hash(m1);
+    }
+  }
+  if (step < nsteps) {  // nsteps even: one step left
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+      hash(m1);
+    }
+  } else if (active) {
+    hash(m0);
+  }
+}
+
 // PROBE (design probes only, K = 10, NXEC_EM_PROBE; outputs are NOT valid):
 // bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
 // the table lookups (parity = first source), to time each role alone.
@@ -254,60 +315,8 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   if (a.hash_prio) __builtin_amdgcn_s_setprio(1);
   const int h = threadIdx.x - kEmCodeLanes;
   const bool active = h < nS * nh;
-  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
   uint32_t st[4];
-  md5_init(st);
-  // The row of step s is read right after barrier s, while the lane hashes
-  // step s - 1 from registers: the reads (queued behind the code waves'
-  // lookups in the LDS) get a whole step to land.  They are complete before
-  // barrier s + 1 (its fence waits for them), so the code waves may refill
-  // that buffer afterwards.
-  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
-    const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
-#pragma unroll
-    for (int i = 0; i < kEmVecs; i++) {
-      const u32x4 x = p[i];
-      m[4 * i] = x.x;
-      m[4 * i + 1] = x.y;
-      m[4 * i + 2] = x.z;
-      m[4 * i + 3] = x.w;
-    }
-  };
-  auto hash = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
-    if (PROBE & 1) {
-#pragma unroll
-      for (int i = 0; i < kEncMd5Step / 4; i++) st[i & 3] ^= m[i];
-    } else {
-#pragma unroll
-      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
-    }
-  };
-  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
-  lds_barrier();
-  if (active) fetch(0, m0);
-  int step = 1;
-  for (; step + 2 <= nsteps; step += 2) {
-    lds_barrier();
-    if (active) {
-      fetch(step, m1);
-      hash(m0);
-    }
-    lds_barrier();
-    if (active) {
-      fetch(step + 1, m0);
-      hash(m1);
-    }
-  }
-  if (step < nsteps) {  // nsteps even: one step left
-    lds_barrier();
-    if (active) {
-      fetch(step, m1);
-      hash(m0);
-      hash(m1);
-    }
-  } else if (active) {
-    hash(m0);
-  }
+  hash_rows<PROBE>(buf, buf_bytes, h, active, nsteps, st);
   if (active) {
     md5_pad_aligned(st, static_cast<uint64_t>(a.len));
     const int ls = h / nh, c = h - ls * nh;
@@ -324,6 +333,122 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
     }
   }
 }
+
+// ring depth of the pointer-table form: as many steps in flight as ~200
+// VGPRs hold (its 64-bit source pointers take 2K of them), at most 8 -- its
+// loads cross PCIe (microseconds each), so small k keeps more steps ahead
+template <int K>
+constexpr int gm_depth() {
+  return (200 - 2 * K) / (16 * K) >= 8 ? 8 : (200 - 2 * K) / (16 * K) < 2 ? 2 : (200 - 2 * K) / (16 * K);
+}
+
+// The agent's requests (container_manager.cc:221-258 partial encodes and
+// agent.cc:240-415 repairs, then the MD5 of every output, agent.cc:342): the
+// same code/hash split as k_mul_md5 with every source and output behind a
+// per-request pointer, so a batch is coded and hashed straight from and into
+// pinned host buffers over PCIe -- no H2D, no D2H, one launch.  Requests are
+// few (tens to ~a thousand) and each is one lane's chain, so a workgroup
+// usually holds fewer requests than it has code lanes: the idle lanes read
+// and write `scratch` in HBM (one address per lane) instead of shadowing a
+// live request, which would multiply its PCIe reads.
+template <int K>
+__global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int nh = a.p;
+  const int S = a.stripes_per_group;
+  uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
+  uint8_t *buf = lds + K * 1024;
+  const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
+  build_tables<1>(a.coef, K, a.p, tab);
+  __syncthreads();
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
+  const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
+  const int nsteps = static_cast<int>(a.len / kEncMd5Step);
+
+  if (threadIdx.x < kEmCodeLanes) {
+    const int item = threadIdx.x;
+    const bool act = item < nS * kEmVecs;
+    const int ls = act ? item / kEmVecs : 0, v = item % kEmVecs;
+    const int64_t sx = s0 + ls;
+    const uint8_t *sp[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) sp[j] = act ? a.src_ptrs[sx * K + j] + v * 16 : a.scratch + v * 16;
+    uint8_t *dp[kMaxRowsPerPass];
+#pragma unroll
+    for (int r = 0; r < kMaxRowsPerPass; r++)
+      dp[r] = act && r < a.p ? a.dst_ptrs[sx * a.p + r] + v * 16 : a.scratch + 256 * (r + 1) + v * 16;
+    const int64_t sstep = act ? kEncMd5Step : 0;  // idle lanes stay on their scratch line
+    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
+    auto load = [&](int step, u32x4(&d)[K]) {
+#pragma unroll
+      for (int j = 0; j < K; j++) d[j] = dev::ld_stream(sp[j] + step * sstep);
+    };
+    auto run = [&](int step, const u32x4(&d)[K]) {
+      uint8_t *rb = row + (step & 1) * buf_bytes;
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
+      }
+      uint32_t o[4][4];
+      rows_of(acc, o);
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++) {
+        if (r < a.p) {  // wave-uniform
+          const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
+          dev::st_stream(dp[r] + step * sstep, pv);
+          if (act) *reinterpret_cast<u32x4 *>(rb + r * kEmRow) = pv;
+        }
+      }
+      lds_barrier();
+    };
+    constexpr int D = gm_depth<K>();
+    u32x4 ring[D][K];
+    const int last = nsteps - 1;
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
+    int step = 0;
+    for (; step + D <= nsteps; step += D) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) {
+      if (step + j < nsteps) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+    return;
+  }
+
+  const int h = threadIdx.x - kEmCodeLanes;
+  const bool active = h < nS * nh;
+  uint32_t st[4];
+  hash_rows<0>(buf, buf_bytes, h, active, nsteps, st);
+  if (active) {
+    md5_pad_aligned(st, static_cast<uint64_t>(a.len));
+    uint32_t *out = reinterpret_cast<uint32_t *>(a.digests + (s0 * nh + h) * 16);  // rows are (request, output) in order
+#pragma unroll
+    for (int i = 0; i < 4; i++) out[i] = st[i];
+  }
+}
+
+using GmKernel = void (*)(const GatherMd5Args);
+template <int... Ks>
+constexpr std::array<GmKernel, sizeof...(Ks)> gm_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_gather_md5<Ks + 1>...}};
+}
+const std::array<GmKernel, kGatherMd5MaxK> kGm = gm_table(std::make_integer_sequence<int, kGatherMd5MaxK>{});
 
 using EmKernel = void (*)(const MulMd5Args);
 template <bool HSRC, int... Ks>
@@ -365,6 +490,13 @@ int prepare_encode_md5() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5): %s", hipGetErrorString(e));
   }
+  for (GmKernel fn : kGm) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
+      return set_error(NXEC_ERR_HIP, "k_gather_md5: static LDS present (the tables must start at LDS byte 0)");
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_gather_md5): %s", hipGetErrorString(e));
+  }
   for (EmKernel fn : kEmProbe) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 probe): %s", hipGetErrorString(e));
@@ -399,6 +531,28 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_mul_md5: %s", hipGetErrorString(e));
+}
+
+int launch_gather_md5(const GatherMd5Args &in, int num_cus, void *stream) {
+  if (in.nstripes <= 0) return NXEC_OK;
+  if (in.k < 1 || in.k > kGatherMd5MaxK || in.p < 1 || in.p > kMaxRowsPerPass || in.len <= 0 ||
+      in.len % kEncMd5Step != 0 || in.len / kEncMd5Step >= (int64_t(1) << 31) || !in.src_ptrs || !in.dst_ptrs ||
+      !in.digests || !in.scratch)
+    return set_error(NXEC_ERR_INVALID, "gather+md5: unsupported arguments");
+  GatherMd5Args a = in;
+  // spread the requests over every CU first (each is one ~9 ms chain per
+  // 1 MiB whatever the batch), then pack up to 16 per workgroup
+  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / a.p);
+  const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
+  if (per_cu < S) S = per_cu;
+  a.stripes_per_group = static_cast<int32_t>(S);
+  const int64_t grid = (a.nstripes + S - 1) / S;
+  if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "gather+md5: batch too large for one launch");
+  const int lds = a.k * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
+  hipLaunchKernelGGL(kGm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_gather_md5: %s", hipGetErrorString(e));
 }
 
 }  // namespace nxec

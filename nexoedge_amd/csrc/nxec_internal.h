@@ -191,6 +191,26 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
 int prepare_encode_md5();
 int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 
+// The agent's form of the fused kernel (nxec_agent_encode_batch): request s
+// reads source j at src_ptrs[s*k + j] and writes output r at dst_ptrs[s*p + r]
+// (device addresses: HBM, or pinned host memory the kernel reads and writes
+// over PCIe), the MD5 of every output to digests + (s*p + r)*16.  scratch: >=
+// 2 KiB of device memory, the target of idle lanes' accesses.  Pointer tables
+// and digests may be device-mapped host memory.  len a positive multiple of
+// kEncMd5Step, every pointer 16-byte aligned.
+constexpr int kGatherMd5MaxK = 16;
+struct GatherMd5Args {
+  const uint8_t *const *src_ptrs;
+  uint8_t *const *dst_ptrs;
+  uint8_t *digests;
+  uint8_t *scratch;
+  int64_t len, nstripes;
+  int32_t k, p;
+  int32_t stripes_per_group;  // set by launch_gather_md5
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
+};
+int launch_gather_md5(const GatherMd5Args &a, int num_cus, void *stream);
+
 }  // namespace nxec
 
 #endif

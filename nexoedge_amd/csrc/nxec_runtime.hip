@@ -1190,6 +1190,11 @@ struct AgentBatch {
   size_t out_off = 0, md5_off = 0;
   int64_t stride = 0;
   size_t d2h_bytes = 0;  // outputs (+ digests) still to be queued device -> host
+  // fused form (k_gather_md5 over pinned memory): the kernel wrote outputs
+  // straight into mapped caller buffers; out_pos[i*no + o] >= 0 is the slot
+  // offset of an output that went to the slot instead (pageable caller buffer)
+  bool fused = false;
+  std::vector<int64_t> out_pos;
 };
 
 // Queues a batch's D2H.  Held back until the next batch's H2D is queued: a
@@ -1223,7 +1228,10 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
     const size_t i = static_cast<size_t>(item / no);
     const int o = item % no;
     const nxec_agent_req &r = reqs[b.reqs[i]];
-    std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * no + o) * b.stride, cs);
+    if (!b.fused)
+      std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * no + o) * b.stride, cs);
+    else if (b.out_pos[static_cast<size_t>(item)] >= 0)
+      std::memcpy(r.outputs[o], b.slot->h + b.out_pos[static_cast<size_t>(item)], cs);
     if (o == 0 && r.md5) std::memcpy(r.md5, b.slot->h + b.md5_off + i * no * 16, size_t(no) * 16);
   });
   b.reqs.clear();
@@ -1237,6 +1245,127 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
 static bool agent_trace() {
   static const bool t = std::getenv("NXEC_AGENT_TRACE") != nullptr;
   return t;
+}
+
+// three staging slots in rotation: batch b gathers into its slot while
+// batch b-1's H2D runs and batch b-2's MD5 chains finish, so the link never
+// waits for a gather (two slots left ~6 ms gaps per batch)
+constexpr int kAgentSlots = 3;
+
+// b's slot holds at least `bytes` (a larger one is taken when it does not)
+static int agent_slot(nxec_ctx_t *ctx, AgentBatch &b, size_t bytes) {
+  bytes = std::max<size_t>(bytes, 4096);
+  if (b.slot && b.slot->cap < bytes) {
+    release_slot(ctx, b.slot);
+    b.slot = nullptr;
+  }
+  return b.slot ? NXEC_OK : acquire_slot(ctx, bytes, &b.slot);
+}
+
+// One matrix group through the fused kernel.  Every input and output is
+// classified once: a pinned / registered caller buffer (an arena Chunk) is
+// handed to the kernel as is, a pageable or misaligned one is gathered into
+// (input) or collected from (output) the slot.  Batches are bounded by the
+// staging they need, not by the bytes they code -- each batch pays one whole
+// MD5 chain (~9 ms per 1 MiB chunk whatever its size), so requests in mapped
+// buffers all go in one launch (64 MiB staging batches: 23 -> 11 GiB/s at one
+// caller).  Slots rotate with the two-kernel form's.
+static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const std::vector<int> &ids,
+                             int64_t chunk_size, int64_t stride, int64_t batch_bytes, AgentBatch (&slots)[kAgentSlots],
+                             int &cur) {
+  const nxec_agent_req &r0 = reqs[ids[0]];
+  const int ni = r0.ninputs, no = r0.noutputs;
+  const size_t nid = ids.size(), cs = size_t(chunk_size);
+  std::vector<uintptr_t> in_dv(nid * ni), out_dv(nid * no);  // 0: not mapped
+  HostPool::get().parallel_for(static_cast<int>(nid * (ni + no)), [&](int item) {
+    const size_t q = static_cast<size_t>(item);
+    if (q < nid * ni) {
+      const unsigned char *p = reqs[ids[q / ni]].inputs[q % ni];
+      in_dv[q] = aligned16(p) ? reinterpret_cast<uintptr_t>(host_device_view_range(p, cs)) : 0;
+    } else {
+      const size_t o = q - nid * ni;
+      unsigned char *p = reqs[ids[o / no]].outputs[o % no];
+      out_dv[o] = aligned16(p) ? reinterpret_cast<uintptr_t>(host_device_view_range(p, cs)) : 0;
+    }
+  });
+  int rc = NXEC_OK;
+  for (size_t first = 0; first < nid && rc == NXEC_OK;) {
+    // [first, last): requests whose staging fits batch_bytes (at least one)
+    size_t last = first;
+    int64_t staged = 0;
+    while (last < nid) {
+      int64_t n_st = 0;
+      for (int j = 0; j < ni; j++) n_st += in_dv[last * ni + j] == 0;
+      for (int o = 0; o < no; o++) n_st += out_dv[last * no + o] == 0;
+      const int64_t need = n_st * stride + int64_t(no) * 16 + (int64_t(ni) + no) * 8;
+      if (last > first && staged + need > batch_bytes) break;
+      staged += need;
+      last++;
+    }
+    const size_t nb = last - first;
+    AgentBatch &b = slots[cur], &other = slots[(cur + kAgentSlots - 1) % kAgentSlots];
+    cur = (cur + 1) % kAgentSlots;
+    const auto tr0 = std::chrono::steady_clock::now();
+    if ((rc = agent_finish(ctx, reqs, chunk_size, b))) break;  // this slot's previous batch
+    const auto tr1 = std::chrono::steady_clock::now();
+    if ((rc = agent_slot(ctx, b, size_t(staged)))) break;
+    uint8_t *hv = static_cast<uint8_t *>(host_device_view(b.slot->h));
+    if (!hv) {
+      rc = set_error(NXEC_ERR_HIP, "agent staging slot is not device-mapped");
+      break;
+    }
+    // slot: [staged chunks][digests nb x no x 16][source table nb x ni][output table nb x no]
+    std::vector<int64_t> in_pos(nb * ni, -1);
+    b.out_pos.assign(nb * no, -1);
+    int64_t pos = 0;
+    for (size_t q = 0; q < nb * ni; q++)
+      if (!in_dv[first * ni + q]) in_pos[q] = pos, pos += stride;
+    for (size_t q = 0; q < nb * no; q++)
+      if (!out_dv[first * no + q]) b.out_pos[q] = pos, pos += stride;
+    b.fused = true;
+    b.stride = stride;
+    b.md5_off = size_t(pos);
+    const size_t tab_off = b.md5_off + nb * no * 16;
+    uint64_t *src_tab = reinterpret_cast<uint64_t *>(b.slot->h + tab_off);
+    uint64_t *dst_tab = src_tab + nb * ni;
+    HostPool::get().parallel_for(static_cast<int>(nb * (ni + no)), [&](int item) {
+      const size_t q = static_cast<size_t>(item);
+      if (q < nb * ni) {
+        if (in_pos[q] < 0) {
+          src_tab[q] = in_dv[first * ni + q];
+        } else {
+          stage_copy(b.slot->h + in_pos[q], reqs[ids[first + q / ni]].inputs[q % ni], cs);
+          src_tab[q] = reinterpret_cast<uintptr_t>(hv + in_pos[q]);
+        }
+      } else {
+        const size_t o = q - nb * ni;
+        dst_tab[o] = b.out_pos[o] < 0 ? out_dv[first * no + o] : reinterpret_cast<uintptr_t>(hv + b.out_pos[o]);
+      }
+    });
+    for (size_t i = first; i < last; i++) b.reqs.push_back(ids[i]);
+    if (agent_trace()) {
+      const auto tr2 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "agent fused batch of %zu (%lld staged bytes): finish-previous %.2f ms, tables + gather %.2f ms\n",
+                   nb, static_cast<long long>(pos), std::chrono::duration<double, std::milli>(tr1 - tr0).count(),
+                   std::chrono::duration<double, std::milli>(tr2 - tr1).count());
+    }
+    GatherMd5Args ga;
+    std::memset(&ga, 0, sizeof(ga));
+    ga.src_ptrs = reinterpret_cast<const uint8_t *const *>(hv + tab_off);
+    ga.dst_ptrs = reinterpret_cast<uint8_t *const *>(hv + tab_off + nb * ni * 8);
+    ga.digests = hv + b.md5_off;
+    ga.scratch = b.slot->d;
+    ga.len = chunk_size;
+    ga.nstripes = int64_t(nb);
+    ga.k = ni;
+    ga.p = no;
+    std::memcpy(ga.coef, r0.matrix, size_t(no) * ni);
+    if ((rc = launch_gather_md5(ga, ctx->num_cus, b.slot->stream))) break;
+    b.d2h_bytes = 0;
+    rc = agent_d2h(ctx, other);  // a two-kernel previous batch's D2H, if any
+    first = last;
+  }
+  return rc;
 }
 
 // One round of agent requests (validated): grouped by matrix, staged through
@@ -1256,10 +1385,19 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
   }
   const int64_t stride = (chunk_size + 15) / 16 * 16;
   if (batch_bytes <= 0) batch_bytes = int64_t(256) << 20;
-  // three staging slots in rotation: batch b gathers into its slot while
-  // batch b-1's H2D runs and batch b-2's MD5 chains finish, so the link never
-  // waits for a gather (two slots left ~6 ms gaps per batch)
-  constexpr int kAgentSlots = 3;
+  if (const char *e = std::getenv("NXEC_AGENT_BATCH_MB")) batch_bytes = std::max<int64_t>(1, std::atoll(e)) << 20;  // tuning
+  // fused form: one k_gather_md5 launch per batch codes and hashes the
+  // requests straight from and into pinned host memory (mapped caller
+  // buffers, e.g. arena Chunks, are used in place; pageable ones go through
+  // the slot).  NXEC_AGENT_FUSED=0: H2D -> multiply -> MD5 -> D2H (A/B).
+  static const bool fused_env = [] {
+    const char *e = std::getenv("NXEC_AGENT_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  static const bool host_direct = [] {
+    const char *e = std::getenv("NXEC_HOST_DIRECT");
+    return !(e && e[0] == '0');
+  }();
   AgentBatch slots[kAgentSlots];
   int cur = 0;
   rc = NXEC_OK;
@@ -1267,8 +1405,16 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     const std::vector<int> &ids = kv.second;
     const nxec_agent_req &r0 = reqs[ids[0]];
     const int ni = r0.ninputs, no = r0.noutputs;
+    bool group_md5 = false;
+    for (int id : ids) group_md5 |= reqs[id].md5 != nullptr;
+    if (fused_env && host_direct && group_md5 && chunk_size % kEncMd5Step == 0 && ni <= kGatherMd5MaxK &&
+        no <= kMaxRowsPerPass) {
+      if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur))) break;
+      continue;
+    }
     const int64_t per = (int64_t(ni) + no) * stride + int64_t(no) * 16;
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));
+    const size_t slot_bytes = size_t(B * per);
     for (size_t first = 0; first < ids.size() && rc == NXEC_OK; first += B) {
       const int64_t nb = std::min<int64_t>(B, int64_t(ids.size() - first));
       AgentBatch &b = slots[cur], &other = slots[(cur + kAgentSlots - 1) % kAgentSlots];
@@ -1276,16 +1422,12 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
       const auto tr0 = std::chrono::steady_clock::now();
       if ((rc = agent_finish(ctx, reqs, chunk_size, b))) break;  // this slot's previous batch
       const auto tr1 = std::chrono::steady_clock::now();
-      if (!b.slot && (rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
-      if (b.slot->cap < size_t(B * per)) {  // grown group: re-acquire a larger slot
-        release_slot(ctx, b.slot);
-        b.slot = nullptr;
-        if ((rc = acquire_slot(ctx, size_t(B * per), &b.slot))) break;
-      }
+      if ((rc = agent_slot(ctx, b, slot_bytes))) break;
       const size_t in_bytes = size_t(nb) * ni * stride;
       b.stride = stride;
       b.out_off = in_bytes;
       b.md5_off = in_bytes + size_t(nb) * no * stride;
+      b.fused = false;
       HostPool::get().parallel_for(static_cast<int>(nb) * ni, [&](int item) {  // gather into pinned staging
         const int64_t i = item / ni;
         const int j = item % ni;
@@ -1335,7 +1477,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
 // taking every queued job of the same chunk size, and runs them as ONE set of
 // batches (one MD5 launch per batch covers all callers' outputs, so the ~10 ms
 // MD5 chain of a 1 MiB chunk is paid once per round, not once per call).
-// Rounds use larger staging (>= 1 GiB per slot) than a lone call.
+// Rounds use larger staging (>= 512 MiB per slot) than a lone call.
 // NXEC_AGENT_AGGREGATE=0 runs every call on its own.
 extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
                                        int64_t batch_bytes) {
@@ -1380,7 +1522,7 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
     }
     lk.unlock();
     std::vector<nxec_agent_req> merged;
-    int64_t bb = int64_t(1) << 30;
+    int64_t bb = int64_t(512) << 20;  // fused form, 4 pageable callers: 20 GiB/s at 1 GiB, 26 at 512 MiB
     for (AgentJob *j : round) {
       merged.insert(merged.end(), j->reqs, j->reqs + j->nreqs);
       bb = std::max(bb, j->batch_bytes);

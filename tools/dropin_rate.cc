@@ -101,6 +101,11 @@ int main(int argc, char **argv) {
       const uint8_t row[4] = {0x1d, 0x3a, 0x74, 0xe8};
       std::vector<int> tlist{1, 4, 16};
       if (const char *e = std::getenv("DROPIN_AGENT_THREADS")) tlist = {std::atoi(e)};
+      // chunk buffers: pageable (the reference's containers malloc them,
+      // fs.cc:180) or arena blocks (an agent whose container reads land in
+      // Chunk::allocateData buffers): the fused kernel then reads and writes
+      // them in place over PCIe
+      for (int arena = 0; arena < 2; arena++)
       for (int threads : tlist) {
         std::atomic<long> calls{0};
         std::atomic<bool> ok{true};
@@ -108,28 +113,48 @@ int main(int argc, char **argv) {
         std::vector<std::thread> pool;
         for (int t = 0; t < threads; t++)
           pool.emplace_back([&, t] {
-            std::vector<uint8_t> in(static_cast<size_t>(nreq) * ni * cs), out(static_cast<size_t>(nreq) * cs),
-                md5(static_cast<size_t>(nreq) * 16);
-            fill(in.data(), in.size(), 5 + t);
+            const size_t in_bytes = static_cast<size_t>(nreq) * ni * cs, out_bytes = static_cast<size_t>(nreq) * cs;
+            std::vector<uint8_t> in_v, out_v, md5(static_cast<size_t>(nreq) * 16);
+            uint8_t *in = nullptr, *out = nullptr;
+            if (arena) {
+              void *a = nullptr, *b = nullptr;
+              if (nxec_host_alloc(in_bytes, &a) != NXEC_OK || nxec_host_alloc(out_bytes, &b) != NXEC_OK) {
+                ok = false;
+                return;
+              }
+              in = static_cast<uint8_t *>(a);
+              out = static_cast<uint8_t *>(b);
+            } else {
+              in_v.resize(in_bytes);
+              out_v.resize(out_bytes);
+              in = in_v.data();
+              out = out_v.data();
+            }
+            fill(in, in_bytes, 5 + t);
             std::vector<const unsigned char *> ip(static_cast<size_t>(nreq) * ni);
             std::vector<unsigned char *> op(nreq);
             std::vector<nxec_agent_req> reqs(nreq);
             for (int r = 0; r < nreq; r++) {
-              for (int j = 0; j < ni; j++) ip[r * ni + j] = in.data() + (static_cast<size_t>(r) * ni + j) * cs;
-              op[r] = out.data() + static_cast<size_t>(r) * cs;
+              for (int j = 0; j < ni; j++) ip[r * ni + j] = in + (static_cast<size_t>(r) * ni + j) * cs;
+              op[r] = out + static_cast<size_t>(r) * cs;
               reqs[r] = {ni, 1, row, ip.data() + r * ni, op.data() + r, md5.data() + r * 16};
             }
             while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < secs) {
               if (nxec_agent_encode_batch(ctx, reqs.data(), nreq, cs, 0) != NXEC_OK) ok = false;
               calls++;
             }
+            if (arena) {
+              nxec_host_free(in);
+              nxec_host_free(out);
+            }
           });
         for (auto &th : pool) th.join();
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         const double bytes = static_cast<double>(calls) * nreq * (ni + 1) * cs;
-        std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes + MD5)\", \"threads\": %d, "
-                    "\"chunk\": %d, \"calls\": %ld, \"GiB_s\": %.2f, \"ms_per_call\": %.3f, \"ok\": %s}\n",
-                    threads, cs, static_cast<long>(calls), bytes / dt / (1 << 30),
+        std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes + MD5)\", \"buffers\": \"%s\", "
+                    "\"threads\": %d, \"chunk\": %d, \"calls\": %ld, \"GiB_s\": %.2f, \"ms_per_call\": %.3f, "
+                    "\"ok\": %s}\n",
+                    arena ? "arena" : "pageable", threads, cs, static_cast<long>(calls), bytes / dt / (1 << 30),
                     1e3 * dt * threads / static_cast<double>(calls), ok ? "true" : "false");
         std::fflush(stdout);
       }
