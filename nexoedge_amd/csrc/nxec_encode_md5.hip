@@ -196,7 +196,8 @@ __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes
 
 // PROBE (design probes only, K = 10, NXEC_EM_PROBE; outputs are NOT valid):
 // bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
-// the table lookups (parity = first source), to time each role alone.
+// the table lookups (parity = first source), bit 2 skips every global load
+// and store (sources made up in registers), to time each role alone.
 // HSRC: the sources are hashed too (write and verified-read paths) -- a
 // template parameter, not a runtime flag: a wave-uniform branch around the
 // sources' LDS writes kept every ring buffer live longer and spilled from
@@ -237,7 +238,12 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
     auto load = [&](int step, u32x4(&d)[K]) {
       const uint32_t off = static_cast<uint32_t>(step) * kEncMd5Step;
 #pragma unroll
-      for (int j = 0; j < K; j++) d[j] = em_load(rsrc_src, vsrc, a.src_off[j] + off);
+      for (int j = 0; j < K; j++) {
+        if (PROBE & 4)  // no HBM traffic: a value the compiler cannot fold
+          d[j] = u32x4{vsrc ^ off, off + j, vsrc, static_cast<uint32_t>(j)};
+        else
+          d[j] = em_load(rsrc_src, vsrc, a.src_off[j] + off);
+      }
     };
     auto run = [&](int step, const u32x4(&d)[K]) {
       uint8_t *rb = row + (step & 1) * buf_bytes;
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          em_store(rsrc_dst, vdst, a.dst_off[r] + off, pv);
+          if (!(PROBE & 4)) em_store(rsrc_dst, vdst, a.dst_off[r] + off, pv);
           if (a.hash_dst) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;
         }
       }
@@ -459,8 +465,9 @@ constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int
 const std::array<EmKernel, kEncMd5MaxK> kEm[2] = {em_table<false>(std::make_integer_sequence<int, kEncMd5MaxK>{}),
                                                   em_table<true>(std::make_integer_sequence<int, kEncMd5MaxK>{})};
 
-const EmKernel kEmProbe[4] = {&k_mul_md5<10, true, 0>, &k_mul_md5<10, true, 1>, &k_mul_md5<10, true, 2>,
-                              &k_mul_md5<10, true, 3>};
+const EmKernel kEmProbe[8] = {&k_mul_md5<10, true, 0>, &k_mul_md5<10, true, 1>, &k_mul_md5<10, true, 2>,
+                              &k_mul_md5<10, true, 3>, &k_mul_md5<10, true, 4>, &k_mul_md5<10, true, 5>,
+                              &k_mul_md5<10, true, 6>, &k_mul_md5<10, true, 7>};
 
 }  // namespace
 
@@ -526,7 +533,7 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   const int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
   if (const char *e = std::getenv("NXEC_EM_PROBE"))
-    if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 3];
+    if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 7];
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
