@@ -12,7 +12,7 @@ CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip \
-            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp \
+            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_device.h $(wildcard $(CSRC)/coding/*.hh)

@@ -502,6 +502,31 @@ int nxec_reset_work_queues(void);
  * coding launch will draw (simulates a launch that died mid-flight). */
 int nxec_debug_poison_next_queue_slot(uint32_t next_tile);
 
+/* ---------------------------------------------------------------------------
+ * 8. Storage-class / proxy INI files, for hosts that drive the coding path
+ *    without the reference's Config singleton (its sample/storage_class.ini
+ *    and proxy.ini).  Same reading as Config (src/common/config.cc):
+ *    classes in file order with exactly one `default = 1` (:267-282), coding
+ *    "rs" case-insensitively (:664-670, :1286-1291), n / k / f -1 when absent
+ *    and values <= 0 read as 0, max_chunk_size 0 when absent and clamped to
+ *    [0, 2^30] (:672-705); misc.repair_using_car of proxy.ini (:320).
+ * ------------------------------------------------------------------------- */
+#define NXEC_CODING_RS 0      /* CodingScheme::RS (define.hh:47-50) */
+#define NXEC_CODING_UNKNOWN 1 /* CodingScheme::UNKNOWN_CODE */
+typedef struct nxec_storage_class {
+  char name[64];
+  int coding;
+  int n, k, f;
+  int64_t max_chunk_size;
+  int is_default;
+} nxec_storage_class;
+/* Classes of the file in file order into out[0 .. min(*count, max)); *count =
+ * number of classes (out may be NULL when max is 0: a sizing call).  NXEC_ERR_INVALID on an unreadable or malformed file,
+ * a class without a boolean `default`, or two default classes. */
+int nxec_storage_classes_load(const char *path, nxec_storage_class *out, int max, int *count);
+/* misc.repair_using_car of a proxy.ini (0 / 1 / true / false) into *car. */
+int nxec_proxy_repair_using_car(const char *path, int *car);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,6 +112,8 @@ _PROTOS = {
     "nxec_host_arena_owns": (C.c_int, [vp]),
     "nxec_host_arena_stats": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "nxec_host_range_mapped": (C.c_int, [vp, C.c_size_t]),
+    "nxec_storage_classes_load": (C.c_int, [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]),
+    "nxec_proxy_repair_using_car": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
     "nxec_reset_work_queues": (C.c_int, []),
     "nxec_debug_poison_next_queue_slot": (C.c_int, [C.c_uint32]),
     "nxec_group_create": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
@@ -123,6 +125,12 @@ _PROTOS = {
     "nxec_group_rs_encode_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, vp]),
     "nxec_group_rs_recover_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, vp]),
 }
+
+
+class StorageClass(C.Structure):
+    """struct nxec_storage_class of include/nxec.h"""
+    _fields_ = [("name", C.c_char * 64), ("coding", C.c_int), ("n", C.c_int), ("k", C.c_int), ("f", C.c_int),
+                ("max_chunk_size", C.c_int64), ("is_default", C.c_int)]
 
 
 class AgentReq(C.Structure):

@@ -1,8 +1,13 @@
 // See coding_options.hh (reference semantics: coding_options.cc:6-60).
 #include "coding_options.hh"
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "nxec.h"
 
 namespace {
 // fixed defaults packed in one word (n | k << 8 | car << 16) so a reader never
@@ -25,6 +30,23 @@ CodingOptions::Defaults CodingOptions::defaults() {
   const uint32_t w = g_fixed.load(std::memory_order_acquire);
   return Defaults{static_cast<coding_param_t>(w & 0xff), static_cast<coding_param_t>((w >> 8) & 0xff),
                   ((w >> 16) & 1u) != 0};
+}
+
+bool CodingOptions::loadDefaults(const char *storageClassIni, const char *proxyIni, const char *storageClass) {
+  int count = 0;
+  if (nxec_storage_classes_load(storageClassIni, nullptr, 0, &count) != NXEC_OK) return false;
+  std::vector<nxec_storage_class> classes(static_cast<size_t>(std::max(count, 1)));
+  if (nxec_storage_classes_load(storageClassIni, classes.data(), static_cast<int>(classes.size()), &count) != NXEC_OK ||
+      count > static_cast<int>(classes.size()))
+    return false;
+  const nxec_storage_class *sc = nullptr;
+  for (int i = 0; i < count; i++)
+    if (storageClass ? std::strcmp(classes[i].name, storageClass) == 0 : classes[i].is_default != 0) sc = &classes[i];
+  if (!sc || sc->n < 1 || sc->k < 1 || sc->n > 255 || sc->k > 255) return false;
+  int car = 0;
+  if (proxyIni && nxec_proxy_repair_using_car(proxyIni, &car) != NXEC_OK) return false;
+  setDefaults(static_cast<coding_param_t>(sc->n), static_cast<coding_param_t>(sc->k), car != 0);
+  return true;
 }
 
 // coding_options.cc:6-11: the reference reads Config here

@@ -48,6 +48,13 @@ class CodingOptions {
   static void setDefaults(coding_param_t n, coding_param_t k, bool repairUsingCAR);
   static void setDefaultsProvider(DefaultsProvider provider);  // nullptr: back to setDefaults' values
   static Defaults defaults();                                  // what CodingOptions() would read now
+  // setDefaults from the reference's INI files without its Config: n and k of
+  // storage class `storageClass` (nullptr: the `default = 1` class) of a
+  // storage_class.ini, the CAR flag from proxy.ini's misc.repair_using_car
+  // (nullptr: off).  false (defaults unchanged) when a file is unreadable or
+  // malformed, the class is missing, or its n / k do not fit coding_param_t.
+  static bool loadDefaults(const char *storageClassIni, const char *proxyIni = nullptr,
+                           const char *storageClass = nullptr);
 
  private:
   coding_param_t _n = 0;

@@ -12,6 +12,7 @@ from typing import Iterable, Optional, Sequence
 
 import numpy as np
 
+from . import _lib
 from ._lib import NXEC_OK, AgentReq, NxecError, check, lib
 
 
@@ -156,6 +157,24 @@ def ec_encode_data(gftbls: np.ndarray, k: int, rows: int, data: Sequence[np.ndar
 
 
 # ------------------------------------------------------------- device side
+def storage_classes(path: str) -> list:
+    """nxec_storage_classes_load: the classes of a storage_class.ini in file order, as dicts
+    (Config's reading, src/common/config.cc:267-282, :664-705)."""
+    count = C.c_int()
+    check(lib.nxec_storage_classes_load(path.encode(), None, 0, C.byref(count)), "nxec_storage_classes_load")
+    arr = (_lib.StorageClass * max(count.value, 1))()
+    check(lib.nxec_storage_classes_load(path.encode(), arr, len(arr), C.byref(count)), "nxec_storage_classes_load")
+    return [{"name": c.name.decode(), "coding": "rs" if c.coding == 0 else "unknown", "n": c.n, "k": c.k, "f": c.f,
+             "max_chunk_size": c.max_chunk_size, "default": bool(c.is_default)} for c in arr[:count.value]]
+
+
+def proxy_repair_using_car(path: str) -> bool:
+    """nxec_proxy_repair_using_car: misc.repair_using_car of a proxy.ini (config.cc:320)."""
+    car = C.c_int()
+    check(lib.nxec_proxy_repair_using_car(path.encode(), C.byref(car)), "nxec_proxy_repair_using_car")
+    return bool(car.value)
+
+
 def device_count() -> int:
     c = C.c_int(0)
     rc = lib.nxec_device_count(C.byref(c))

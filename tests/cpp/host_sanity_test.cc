@@ -15,10 +15,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "coding/coding_generator.hh"
+#include "coding/coding_options.hh"
 #include "coding/coding_util.hh"
 #include "nxec.h"
 
@@ -175,9 +179,57 @@ static void surface(int tid) {
   delete code;
 }
 
+// the INI reader of include/nxec.h §8 (Config's reading of the sample files)
+static std::string write_tmp(const char *text) {
+  char path[] = "/tmp/nxec_ini_XXXXXX";
+  const int fd = mkstemp(path);
+  if (fd < 0) return std::string();
+  const ssize_t w = write(fd, text, std::strlen(text));
+  close(fd);
+  return w == static_cast<ssize_t>(std::strlen(text)) ? std::string(path) : std::string();
+}
+
+static void ini_files() {
+  const std::string sc = write_tmp(
+      "[standard]\n; comment\ndefault = 1\ncoding = rs\nn = 4\nk = 2\nf = 1\nmax_chunk_size = 4194304\n\n"
+      "[wide]\n# other comment\n  default=0\ncoding = RS\nn = 14\nk = 10\nf = 99999999999\nmax_chunk_size = 2000000000\n"
+      "[odd]\ndefault = false\ncoding = lrc\nn = -3\n");
+  nxec_storage_class c[4];
+  int count = 0;
+  CHECK(nxec_storage_classes_load(sc.c_str(), c, 4, &count) == NXEC_OK && count == 3, "three classes");
+  CHECK(std::strcmp(c[0].name, "standard") == 0 && c[0].is_default && c[0].coding == NXEC_CODING_RS && c[0].n == 4 &&
+            c[0].k == 2 && c[0].f == 1 && c[0].max_chunk_size == 4194304,
+        "sample class");
+  CHECK(!c[1].is_default && c[1].coding == NXEC_CODING_RS && c[1].n == 14 && c[1].f == -1 &&
+            c[1].max_chunk_size == (int64_t(1) << 30),
+        "clamped max_chunk_size, out-of-int f falls back to its default");
+  CHECK(c[2].coding == NXEC_CODING_UNKNOWN && c[2].n == 0 && c[2].k == -1, "unknown coding, n <= 0 reads 0");
+  CHECK(nxec_storage_classes_load(sc.c_str(), nullptr, 0, &count) == NXEC_OK && count == 3, "sizing call");
+  const std::string two = write_tmp("[a]\ndefault = 1\n[b]\ndefault = 1\n");
+  CHECK(nxec_storage_classes_load(two.c_str(), c, 4, &count) == NXEC_ERR_INVALID, "two defaults rejected");
+  const std::string bad = write_tmp("[a]\ndefault = 1\njunk line\n");
+  CHECK(nxec_storage_classes_load(bad.c_str(), c, 4, &count) == NXEC_ERR_INVALID, "malformed line rejected");
+  const std::string dup = write_tmp("[a]\ndefault = 1\nn = 1\nn = 2\n");
+  CHECK(nxec_storage_classes_load(dup.c_str(), c, 4, &count) == NXEC_ERR_INVALID, "duplicate key rejected");
+  CHECK(nxec_storage_classes_load("/nonexistent/storage_class.ini", c, 4, &count) == NXEC_ERR_INVALID, "missing file");
+  const std::string px = write_tmp("[proxy]\nnum_proxy = 1\n[misc]\nrepair_at_proxy = 1\nrepair_using_car = 1\n");
+  int car = 0;
+  CHECK(nxec_proxy_repair_using_car(px.c_str(), &car) == NXEC_OK && car == 1, "CAR flag");
+  CHECK(CodingOptions::loadDefaults(sc.c_str(), px.c_str()) && CodingOptions::defaults().n == 4 &&
+            CodingOptions::defaults().k == 2 && CodingOptions::defaults().repairUsingCAR,
+        "defaults from the default class");
+  CHECK(CodingOptions::loadDefaults(sc.c_str(), nullptr, "wide") && CodingOptions().getN() == 14 &&
+            CodingOptions().getK() == 10 && !CodingOptions().repairUsingCAR(),
+        "defaults from a named class");
+  CHECK(!CodingOptions::loadDefaults(sc.c_str(), nullptr, "odd") && CodingOptions().getN() == 14, "invalid n kept old");
+  CodingOptions::setDefaults(0, 0, false);
+  for (const std::string &f : {sc, two, bad, dup, px}) unlink(f.c_str());
+}
+
 int main() {
   gf_and_planning();
   argument_validation();
+  ini_files();
   std::vector<std::thread> th;
   for (int t = 0; t < 8; t++) th.emplace_back(surface, t);
   for (auto &t : th) t.join();
