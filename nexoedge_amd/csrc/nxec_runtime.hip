@@ -1277,6 +1277,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
   const int ni = r0.ninputs, no = r0.noutputs;
   const size_t nid = ids.size(), cs = size_t(chunk_size);
   std::vector<uintptr_t> in_dv(nid * ni), out_dv(nid * no);  // 0: not mapped
+  const auto tc0 = std::chrono::steady_clock::now();
   HostPool::get().parallel_for(static_cast<int>(nid * (ni + no)), [&](int item) {
     const size_t q = static_cast<size_t>(item);
     if (q < nid * ni) {
@@ -1288,6 +1289,9 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       out_dv[o] = aligned16(p) ? reinterpret_cast<uintptr_t>(host_device_view_range(p, cs)) : 0;
     }
   });
+  if (agent_trace())
+    std::fprintf(stderr, "agent fused group of %zu: classify %zu buffers %.3f ms\n", nid, nid * (ni + no),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
   int rc = NXEC_OK;
   for (size_t first = 0; first < nid && rc == NXEC_OK;) {
     // [first, last): requests whose staging fits batch_bytes (at least one)
