@@ -218,6 +218,14 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   const int nsteps = static_cast<int>(a.len / kEncMd5Step);
 
   if (threadIdx.x < kEmCodeLanes) {
+    // A code wave with no live stripe (S * 16 < 256 lanes: fewer stripes per
+    // workgroup than it has code lanes) only keeps the step barriers; running
+    // it as a shadow would repeat a live wave's loads and LDS lookups, and the
+    // lookups are the code role's bound (bank conflicts).
+    if ((threadIdx.x & ~63) >= nS * kEmVecs) {
+      for (int s = 0; s < nsteps; s++) lds_barrier();
+      return;
+    }
     // ---- code waves: lane = (stripe ls, column vector v) ----
     // Lanes past the group's last stripe (a partial last group) shadow lane
     // (0, v): same loads, same values stored to the same places.  Everything
@@ -372,6 +380,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
   const int nsteps = static_cast<int>(a.len / kEncMd5Step);
 
   if (threadIdx.x < kEmCodeLanes) {
+    if ((threadIdx.x & ~63) >= nS * kEmVecs) {  // no live request in this wave: barriers only
+      for (int s = 0; s < nsteps; s++) lds_barrier();
+      return;
+    }
     const int item = threadIdx.x;
     const bool act = item < nS * kEmVecs;
     const int ls = act ? item / kEmVecs : 0, v = item % kEmVecs;
