@@ -707,6 +707,11 @@ def main():
             k, cs = args.k, args.chunk
             result["user_data_gib_s"] = round(2 * wl.stripes * k * cs * args.steps * world / elapsed / GIB, 2)
     headline_n1 = rank == 0 and world == 1 and wl.name == "rs10_4"
+    if args.host_inclusive and world > 1 and wl.name == "rs10_4":
+        # every rank at once: the host-resident encode over each GPU's own link
+        hi = host_inclusive_ranks(ctx, grp, args.n, args.k, args.chunk)
+        if rank == 0:
+            result["host_inclusive"] = hi
     if args.host_inclusive and headline_n1:
         result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
     if headline_n1 and not args.no_cpu_baseline:
@@ -775,6 +780,45 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     out["read_frames_decode_GiB_s_user_data"] = round(read_from_frames(ctx, n, k, cs, min(ns, 128)), 2)
     out["recover_frames_zero_copy"] = recover_frames_rate(ctx, n, k, cs, min(ns, 128))
     return out
+
+
+def host_inclusive_ranks(ctx, grp, n, k, cs, ns=256, reps=3):
+    """N > 1: every rank runs the zero-copy host-batch encode (pinned data in,
+    pinned parity out, its own GPU's PCIe link) at the same time, between two
+    barriers; aggregate = all ranks' (k+p)*cs / the slowest rank's time.  A
+    rank whose leg fails still joins every collective (reports -1), so one
+    failure cannot hang the others."""
+    p = n - k
+    t, bufs = -1.0, []
+    try:
+        bufs.append(nxec.PinnedBuffer(ns * k * cs))
+        bufs.append(nxec.PinnedBuffer(ns * p * cs))
+        hd, hp = bufs
+        hd.array[:] = 0x5A
+        ctx.rs_encode_host_batch(n, k, hd.ptr, hp.ptr, cs, ns, 64)  # warm
+        ready = True
+    except Exception:  # noqa: BLE001  (reported, not raised: the ranks must stay in step)
+        ready = False
+    grp.barrier()
+    if ready:
+        try:
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.rs_encode_host_batch(n, k, hd.ptr, hp.ptr, cs, ns, 64)
+            t = (time.perf_counter() - t0) / reps
+        except Exception:  # noqa: BLE001
+            t = -1.0
+    grp.barrier()
+    failed = grp.sum(1.0 if t <= 0 else 0.0)
+    tmax = grp.max(t)
+    for b in bufs:
+        b.free()
+    if failed:
+        return {"error": f"{int(failed)} rank(s) failed the host-inclusive leg"}
+    agg = grp.world * ns * (k + p) * cs / tmax / GIB
+    return {"encode_GiB_s_(k+p)cs_all_ranks": round(agg, 2), "per_rank_GiB_s": round(agg / grp.world, 2),
+            "ranks": grp.world, "stripes_per_rank": ns, "batch": 64,
+            "note": "zero copy over each GPU's own PCIe link, all ranks at once (slowest rank's time)"}
 
 
 def read_from_frames(ctx, n, k, cs, ns, readers=1):
