@@ -141,9 +141,13 @@ __device__ __forceinline__ void lds_barrier() {
 // waits for them), so the code waves may refill that buffer afterwards.
 // Every hash wave takes part in every barrier; st is the state after the
 // last data block (not yet padded).  PROBE bit 0: XOR instead of MD5 rounds.
-template <int PROBE>
+// TAIL: the last step holds `tail` bytes (1..kEncMd5Step; the code lanes
+// zeroed the rest of its row) of a `len`-byte chunk, and st comes back
+// finished -- the step's full blocks, then the padding block(s) of RFC 1321
+// §3.1-3.2 built in registers from the row.
+template <int PROBE, bool TAIL = false>
 __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes, int h, bool active, int nsteps,
-                                          uint32_t (&st)[4]) {
+                                          uint32_t (&st)[4], int tail = kEncMd5Step, uint64_t len = 0) {
   const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
   md5_init(st);
   auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
@@ -164,6 +168,39 @@ __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes
     } else {
 #pragma unroll
       for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+    }
+  };
+  auto hash_last = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
+    if (!TAIL) {
+      hash(m);
+      return;
+    }
+    const int fb = tail / 64, r = tail % 64;  // uniform: one chunk size per launch
+#pragma unroll
+    for (int b = 0; b < kEncMd5Step / 64; b++)
+      if (b < fb) md5_block(st, m + 16 * b);
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++)
+        if (b == fb) x = m[16 * b + i];  // the partial block (none when fb == 4)
+      w[i] = x | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
+    }
+    const uint32_t lo = static_cast<uint32_t>(len * 8), hi = static_cast<uint32_t>((len * 8) >> 32);
+    if (r < 56) {
+      w[14] = lo;
+      w[15] = hi;
+      md5_block(st, w);
+    } else {
+      md5_block(st, w);
+      uint32_t z[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) z[i] = 0;
+      z[14] = lo;
+      z[15] = hi;
+      md5_block(st, z);
     }
   };
   uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
@@ -187,10 +224,10 @@ __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes
     if (active) {
       fetch(step, m1);
       hash(m0);
-      hash(m1);
+      hash_last(m1);
     }
   } else if (active) {
-    hash(m0);
+    hash_last(m0);
   }
 }
 
@@ -377,7 +414,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
   __syncthreads();
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
   const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
-  const int nsteps = static_cast<int>(a.len / kEncMd5Step);
+  // any length: nfull whole steps, then a partial step of `tail` bytes
+  const int nfull = static_cast<int>(a.len / kEncMd5Step);
+  const int tail = static_cast<int>(a.len - static_cast<int64_t>(nfull) * kEncMd5Step);
+  const int nsteps = nfull + (tail > 0);
 
   if (threadIdx.x < kEmCodeLanes) {
     if ((threadIdx.x & ~63) >= nS * kEmVecs) {  // no live request in this wave: barriers only
@@ -425,26 +465,69 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
       lds_barrier();
     };
     constexpr int D = gm_depth<K>();
-    u32x4 ring[D][K];
-    const int last = nsteps - 1;
+    if (nfull > 0) {  // the whole steps through the ring (uniform branch)
+      u32x4 ring[D][K];
+      const int last = nfull - 1;
 #pragma unroll
-    for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
-    int step = 0;
-    for (; step + D <= nsteps; step += D) {
+      for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
+      int step = 0;
+      for (; step + D <= nfull; step += D) {
 #pragma unroll
-      for (int j = 0; j < D; j++) {
-        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
-        __builtin_amdgcn_sched_barrier(0);
-        run(step + j, ring[j]);
+        for (int j = 0; j < D; j++) {
+          load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+          __builtin_amdgcn_sched_barrier(0);
+          run(step + j, ring[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < D - 1; j++) {
+        if (step + j < nfull) {
+          load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+          __builtin_amdgcn_sched_barrier(0);
+          run(step + j, ring[j]);
+        }
       }
     }
+    if (tail > 0) {
+      // the partial last step: nothing past a chunk's end is read or written
+      // (a caller's buffer may end at a page); a lane straddling the end moves
+      // its bytes one at a time, lanes past it load zeros and store nothing,
+      // so the step's LDS row is zero-padded for the hash lanes
+      const int nb = act ? min(max(tail - v * 16, 0), 16) : 16;  // idle lanes: their scratch line
+      const int64_t off = static_cast<int64_t>(nfull) * sstep;
+      u32x4 d[K];
 #pragma unroll
-    for (int j = 0; j < D - 1; j++) {
-      if (step + j < nsteps) {
-        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
-        __builtin_amdgcn_sched_barrier(0);
-        run(step + j, ring[j]);
+      for (int j = 0; j < K; j++) {
+        if (nb == 16) {
+          d[j] = dev::ld_stream(sp[j] + off);
+        } else {
+          uint32_t w[4] = {0, 0, 0, 0};
+          for (int i = 0; i < nb; i++) w[i / 4] |= static_cast<uint32_t>(sp[j][off + i]) << (8 * (i % 4));
+          d[j] = u32x4{w[0], w[1], w[2], w[3]};
+        }
       }
+      uint8_t *rb = row + (nfull & 1) * buf_bytes;
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int j = 0; j < K; j += 2) lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+      uint32_t o[4][4];
+      rows_of(acc, o);
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++) {
+        if (r < a.p) {
+          const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
+          if (nb == 16) {
+            dev::st_stream(dp[r] + off, pv);
+          } else {
+            const uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
+            for (int i = 0; i < nb; i++) dp[r][off + i] = static_cast<uint8_t>(w[i / 4] >> (8 * (i % 4)));
+          }
+          if (act) *reinterpret_cast<u32x4 *>(rb + r * kEmRow) = pv;  // zero past the end: GF products of zeros
+        }
+      }
+      lds_barrier();
     }
     return;
   }
@@ -452,9 +535,9 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
   const int h = threadIdx.x - kEmCodeLanes;
   const bool active = h < nS * nh;
   uint32_t st[4];
-  hash_rows<0>(buf, buf_bytes, h, active, nsteps, st);
+  hash_rows<0, true>(buf, buf_bytes, h, active, nsteps, st, tail > 0 ? tail : kEncMd5Step,
+                     static_cast<uint64_t>(a.len));
   if (active) {
-    md5_pad_aligned(st, static_cast<uint64_t>(a.len));
     uint32_t *out = reinterpret_cast<uint32_t *>(a.digests + (s0 * nh + h) * 16);  // rows are (request, output) in order
 #pragma unroll
     for (int i = 0; i < 4; i++) out[i] = st[i];
@@ -555,8 +638,7 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
 int launch_gather_md5(const GatherMd5Args &in, int num_cus, void *stream) {
   if (in.nstripes <= 0) return NXEC_OK;
   if (in.k < 1 || in.k > kGatherMd5MaxK || in.p < 1 || in.p > kMaxRowsPerPass || in.len <= 0 ||
-      in.len % kEncMd5Step != 0 || in.len / kEncMd5Step >= (int64_t(1) << 31) || !in.src_ptrs || !in.dst_ptrs ||
-      !in.digests || !in.scratch)
+      in.len / kEncMd5Step >= (int64_t(1) << 31) - 1 || !in.src_ptrs || !in.dst_ptrs || !in.digests || !in.scratch)
     return set_error(NXEC_ERR_INVALID, "gather+md5: unsupported arguments");
   GatherMd5Args a = in;
   // spread the requests over every CU first (each is one ~9 ms chain per

@@ -196,8 +196,8 @@ int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 // (device addresses: HBM, or pinned host memory the kernel reads and writes
 // over PCIe), the MD5 of every output to digests + (s*p + r)*16.  scratch: >=
 // 2 KiB of device memory, the target of idle lanes' accesses.  Pointer tables
-// and digests may be device-mapped host memory.  len a positive multiple of
-// kEncMd5Step, every pointer 16-byte aligned.
+// and digests may be device-mapped host memory.  Any len > 0 (a partial last
+// step never touches bytes past a chunk's end); every pointer 16-byte aligned.
 constexpr int kGatherMd5MaxK = 16;
 struct GatherMd5Args {
   const uint8_t *const *src_ptrs;

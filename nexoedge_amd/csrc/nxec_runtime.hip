@@ -1390,7 +1390,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
   const int64_t stride = (chunk_size + 15) / 16 * 16;
   if (batch_bytes <= 0) batch_bytes = int64_t(256) << 20;
   if (const char *e = std::getenv("NXEC_AGENT_BATCH_MB")) batch_bytes = std::max<int64_t>(1, std::atoll(e)) << 20;  // tuning
-  // fused form: one k_gather_md5 launch per batch codes and hashes the
+  // fused form (any chunk size): one k_gather_md5 launch per batch codes and hashes the
   // requests straight from and into pinned host memory (mapped caller
   // buffers, e.g. arena Chunks, are used in place; pageable ones go through
   // the slot).  NXEC_AGENT_FUSED=0: H2D -> multiply -> MD5 -> D2H (A/B).
@@ -1411,8 +1411,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     const int ni = r0.ninputs, no = r0.noutputs;
     bool group_md5 = false;
     for (int id : ids) group_md5 |= reqs[id].md5 != nullptr;
-    if (fused_env && host_direct && group_md5 && chunk_size % kEncMd5Step == 0 && ni <= kGatherMd5MaxK &&
-        no <= kMaxRowsPerPass) {
+    if (fused_env && host_direct && group_md5 && ni <= kGatherMd5MaxK && no <= kMaxRowsPerPass) {
       if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur))) break;
       continue;
     }

@@ -106,8 +106,46 @@ def test_agent_fused_many_requests_packed_per_workgroup(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_agent_unaligned_chunk_size_keeps_two_kernel_form(gpu_ctx):
-    """cs not a multiple of 256 (or no digest requested at all): the
-    H2D -> multiply -> MD5 -> D2H form, same results."""
-    run_batch(gpu_ctx, [(4, 1), (12, 2)], 65536 + 16, "arena", "pageable", nreq=6, seed=5)
+@pytest.mark.parametrize("cs", [1, 15, 16, 17, 100, 255, 257, 319, 5000, 65536 + 16, (1 << 20) - 3])
+def test_agent_fused_any_chunk_size(gpu_ctx, cs):
+    """Chunk sizes that are not a multiple of the 256-byte step (a file's last
+    stripe, ceil(rem/k) bytes): the partial last step reads and writes nothing
+    past a chunk's end -- every output sits in a larger buffer whose bytes past
+    cs must keep their sentinel -- and the MD5 padding is built in registers."""
+    rng = np.random.default_rng(cs)
+    arena = Arena()
+    try:
+        reqs, want, guards = [], [], []
+        for r in range(6):
+            ni, no = [(4, 1), (12, 2), (3, 1)][r % 3]
+            m = rng.integers(0, 256, size=(no, ni), dtype=np.uint8)
+            ins = []
+            for j in range(ni):
+                a = make_buf(arena, ("arena", "pageable")[(r + j) % 2], cs, r)
+                a[:] = rng.integers(0, 256, size=cs, dtype=np.uint8)
+                ins.append(a)
+            outs, g = [], []
+            for o in range(no):
+                big = arena.array(cs + 64) if (r + o) % 2 == 0 else np.zeros(cs + 64, dtype=np.uint8)
+                big[:] = 0xEE
+                outs.append(big[:cs])
+                g.append(big)
+            md5 = np.zeros((no, 16), dtype=np.uint8)
+            reqs.append((m, ins, outs, md5))
+            want.append(oracle.matmul(m, [x.copy() for x in ins]))
+            guards.append(g)
+        gpu_ctx.agent_encode_batch(reqs, cs)
+        for r, ((m, ins, outs, md5), w, g) in enumerate(zip(reqs, want, guards)):
+            for o in range(m.shape[0]):
+                assert np.array_equal(outs[o], w[o]), (r, o)
+                assert md5[o].tobytes().hex() == hashlib.md5(w[o].tobytes()).hexdigest(), (r, o)
+                assert (g[o][cs:] == 0xEE).all(), (r, o)  # nothing written past the chunk
+    finally:
+        arena.free()
+
+
+@pytest.mark.gpu
+def test_agent_without_digests_keeps_two_kernel_form(gpu_ctx):
+    """A group that asks for no digest at all runs H2D -> multiply -> D2H."""
     run_batch(gpu_ctx, [(4, 1)], 65536, "arena", "arena", nreq=6, seed=6, with_md5=lambda r: False)
+    run_batch(gpu_ctx, [(4, 1), (12, 2)], 65536 + 16, "arena", "pageable", nreq=6, seed=5, with_md5=lambda r: False)
