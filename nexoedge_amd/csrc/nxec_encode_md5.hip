@@ -544,6 +544,203 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
   }
 }
 
+// Hash waves of k_files_md5: hash_rows with a length per lane.  Lane h's
+// chunk has my_steps steps, the last holding my_tail bytes (1..256; the row is
+// zero past them); the workgroup runs nsteps >= my_steps steps (its longest
+// request), and a lane that is done only keeps the barriers.  st comes back
+// finished (RFC 1321 padding built in registers).
+__device__ __forceinline__ void hash_rows_var(const uint8_t *buf, uint32_t buf_bytes, int h, bool active, int nsteps,
+                                              int my_steps, int my_tail, uint64_t len, uint32_t (&st)[4]) {
+  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
+  md5_init(st);
+  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
+    const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
+#pragma unroll
+    for (int i = 0; i < kEmVecs; i++) {
+      const u32x4 x = p[i];
+      m[4 * i] = x.x;
+      m[4 * i + 1] = x.y;
+      m[4 * i + 2] = x.z;
+      m[4 * i + 3] = x.w;
+    }
+  };
+  auto proc = [&](int t, const uint32_t(&m)[kEncMd5Step / 4]) {
+    if (!active || t >= my_steps) return;
+    if (t < my_steps - 1) {
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+      return;
+    }
+    const int fb = my_tail / 64, r = my_tail % 64;
+#pragma unroll
+    for (int b = 0; b < kEncMd5Step / 64; b++)
+      if (b < fb) md5_block(st, m + 16 * b);
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++)
+        if (b == fb) x = m[16 * b + i];
+      w[i] = x | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
+    }
+    const uint32_t lo = static_cast<uint32_t>(len * 8), hi = static_cast<uint32_t>((len * 8) >> 32);
+    if (r >= 56) {
+      md5_block(st, w);
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = 0;
+    }
+    w[14] = lo;
+    w[15] = hi;
+    md5_block(st, w);
+  };
+  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
+  lds_barrier();
+  if (active) fetch(0, m0);
+  int step = 1;
+  for (; step + 2 <= nsteps; step += 2) {
+    lds_barrier();
+    if (active && step < my_steps) fetch(step, m1);
+    proc(step - 1, m0);
+    lds_barrier();
+    if (active && step + 1 < my_steps) fetch(step + 1, m0);
+    proc(step, m1);
+  }
+  if (step < nsteps) {
+    lds_barrier();
+    if (active && step < my_steps) fetch(step, m1);
+    proc(step - 1, m0);
+    proc(step, m1);
+  } else {
+    proc(step - 1, m0);
+  }
+}
+
+// The multi-file write in one launch (nxec_encode_objects; the per-file
+// loop of Proxy::writeFileStripes, proxy_file_ops.cc:557-666, with
+// writeFileStripe's encode + Chunk::computeMD5 of all n chunks,
+// chunk_manager.cc:66-452): k_mul_md5's code/hash split over pointer tables,
+// every request (a full stripe read in place from its object, or a file's
+// zero-padded last stripe in the tail arena) with its own chunk length.
+// Requests come sorted longest first, so a workgroup's first request sets its
+// step count; a lane past its request's end re-reads its last in-bounds
+// vector, stores to scratch and leaves zeros in its LDS row.
+template <int K>
+__global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
+  extern __shared__ __align__(16) uint8_t lds[];
+  const int nh = K + a.p;
+  const int S = a.stripes_per_group;
+  uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
+  uint8_t *buf = lds + K * 1024;
+  const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
+  build_tables<1>(a.coef, K, a.p, tab);
+  __syncthreads();
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
+  const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
+  const int nsteps = static_cast<int>((a.lens[s0] + kEncMd5Step - 1) / kEncMd5Step);
+
+  if (threadIdx.x < kEmCodeLanes) {
+    if ((threadIdx.x & ~63) >= nS * kEmVecs) {  // no live request in this wave: barriers only
+      for (int s = 0; s < nsteps; s++) lds_barrier();
+      return;
+    }
+    const int item = threadIdx.x;
+    const bool act = item < nS * kEmVecs;
+    const int ls = act ? item / kEmVecs : 0, v = item % kEmVecs;
+    const int64_t sx = s0 + ls;
+    const int64_t vlen = act ? (a.lens[sx] + 15) / 16 * 16 : 0;
+    // last step with bytes of this lane's column (-1: none)
+    const int tmax = vlen > v * 16 ? static_cast<int>((vlen - 1 - v * 16) / kEncMd5Step) : -1;
+    const int tcl = tmax < 0 ? 0 : tmax;
+    const uint8_t *sp[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) sp[j] = tmax >= 0 ? a.src_ptrs[sx * K + j] + v * 16 : a.scratch + v * 16;
+    uint8_t *dp[kMaxRowsPerPass];
+#pragma unroll
+    for (int r = 0; r < kMaxRowsPerPass; r++)
+      dp[r] = tmax >= 0 && r < a.p ? a.dst_ptrs[sx * a.p + r] + v * 16 : a.scratch + 256 * (r + 1) + v * 16;
+    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
+    const u32x4 zero{0u, 0u, 0u, 0u};
+    auto load = [&](int step, u32x4(&d)[K]) {
+      const int64_t off = static_cast<int64_t>(min(step, tcl)) * kEncMd5Step;
+#pragma unroll
+      for (int j = 0; j < K; j++) d[j] = dev::ld_stream(sp[j] + off);
+    };
+    auto run = [&](int step, const u32x4(&d)[K]) {
+      const bool ok = step <= tmax;
+      uint8_t *rb = row + (step & 1) * buf_bytes;
+      uint32_t acc[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        if (act) {
+          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = ok ? d[j] : zero;
+          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = ok ? d[j + 1] : zero;
+        }
+        lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+#pragma unroll
+        for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
+      }
+      uint32_t o[4][4];
+      rows_of(acc, o);
+      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++) {
+        if (r < a.p) {  // wave-uniform
+          const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
+          dev::st_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
+          if (act) *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = ok ? pv : zero;
+        }
+      }
+      lds_barrier();
+    };
+    constexpr int D = gm_depth<K>();
+    u32x4 ring[D][K];
+    const int last = nsteps - 1;
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
+    int step = 0;
+    for (; step + D <= nsteps; step += D) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) {
+      if (step + j < nsteps) {
+        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        run(step + j, ring[j]);
+      }
+    }
+    return;
+  }
+
+  const int h = threadIdx.x - kEmCodeLanes;
+  const bool active = h < nS * nh;
+  const int64_t my_len = active ? a.lens[s0 + h / nh] : 1;
+  const int my_steps = static_cast<int>((my_len + kEncMd5Step - 1) / kEncMd5Step);
+  const int my_tail = static_cast<int>(my_len - static_cast<int64_t>(my_steps - 1) * kEncMd5Step);
+  uint32_t st[4];
+  hash_rows_var(buf, buf_bytes, h, active, nsteps, my_steps, my_tail, static_cast<uint64_t>(my_len), st);
+  if (active) {
+    uint8_t *out = a.dig_ptrs[s0 + h / nh] + (h % nh) * 16;
+#pragma unroll
+    for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+  }
+}
+
+using FmKernel = void (*)(const FilesMd5Args);
+template <int... Ks>
+constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int, Ks...>) {
+  return {{&k_files_md5<Ks + 1>...}};
+}
+const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+
 using GmKernel = void (*)(const GatherMd5Args);
 template <int... Ks>
 constexpr std::array<GmKernel, sizeof...(Ks)> gm_table(std::integer_sequence<int, Ks...>) {
@@ -592,6 +789,13 @@ int prepare_encode_md5() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5): %s", hipGetErrorString(e));
   }
+  for (FmKernel fn : kFm) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
+      return set_error(NXEC_ERR_HIP, "k_files_md5: static LDS present (the tables must start at LDS byte 0)");
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5): %s", hipGetErrorString(e));
+  }
   for (GmKernel fn : kGm) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
@@ -633,6 +837,26 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_mul_md5: %s", hipGetErrorString(e));
+}
+
+int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
+  if (in.nstripes <= 0) return NXEC_OK;
+  if (in.k < 1 || in.k > kFilesMd5MaxK || in.p < 1 || in.p > kMaxRowsPerPass || !in.src_ptrs || !in.dst_ptrs ||
+      !in.lens || !in.dig_ptrs || !in.scratch)
+    return set_error(NXEC_ERR_INVALID, "files+md5: unsupported arguments");
+  FilesMd5Args a = in;
+  const int nh = a.k + a.p;
+  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / nh);
+  const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
+  if (per_cu < S) S = per_cu;
+  a.stripes_per_group = static_cast<int32_t>(S);
+  const int64_t grid = (a.nstripes + S - 1) / S;
+  if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
+  const int lds = a.k * 1024 + static_cast<int>(2 * S * nh * kEmRow);
+  hipLaunchKernelGGL(kFm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
+                     static_cast<hipStream_t>(stream), a);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_files_md5: %s", hipGetErrorString(e));
 }
 
 int launch_gather_md5(const GatherMd5Args &in, int num_cus, void *stream) {

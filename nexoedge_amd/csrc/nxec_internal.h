@@ -211,6 +211,27 @@ struct GatherMd5Args {
 };
 int launch_gather_md5(const GatherMd5Args &a, int num_cus, void *stream);
 
+// The multi-file write in one launch (nxec_encode_objects): request s codes
+// k sources src_ptrs[s*k + j] into p outputs dst_ptrs[s*p + r] and hashes
+// all k + p chunks, lens[s] bytes each, digest of chunk c (sources first) at
+// dig_ptrs[s] + c*16.  Bytes up to the next multiple of 16 past lens[s] are
+// readable (and zero for a zero-padded last stripe); outputs are written up
+// to that multiple.  Requests sorted by length, longest first.  Every
+// pointer 16-byte aligned (digests any); tables in device memory.
+constexpr int kFilesMd5MaxK = 16;
+struct FilesMd5Args {
+  const uint8_t *const *src_ptrs;
+  uint8_t *const *dst_ptrs;
+  const int64_t *lens;
+  uint8_t *const *dig_ptrs;
+  uint8_t *scratch;  // >= 2 KiB of device memory: idle lanes' loads / stores
+  int64_t nstripes;
+  int32_t k, p;
+  int32_t stripes_per_group;  // set by launch_files_md5
+  uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
+};
+int launch_files_md5(const FilesMd5Args &a, int num_cus, void *stream);
+
 }  // namespace nxec
 
 #endif

@@ -953,6 +953,15 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   // ragged stripes through the aligned work-queue kernel: parity slots must be
   // 16-byte aligned (else they join the byte-capable list kernel)
   const bool ragged_ok = p > 0 && M % 16 == 0 && (reinterpret_cast<uintptr_t>(d_parity) & 15) == 0 && k <= kMaxRaggedK;
+  // one launch for every stripe's coding and every chunk's MD5 (k_files_md5):
+  // full stripes in place, last stripes from the tail arena after the pad copy
+  // (NXEC_FUSED_MD5=0: the separate launches, for A/B)
+  const char *fenv = std::getenv("NXEC_FUSED_MD5");
+  const bool want_fused = !(fenv && fenv[0] == '0') && d_md5 && ragged_ok && p <= kMaxRowsPerPass &&
+                          k <= kFilesMd5MaxK;
+  std::vector<const uint8_t *> q_src;
+  std::vector<uint8_t *> q_dst, q_dig;
+  std::vector<int64_t> q_len;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
@@ -965,6 +974,12 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
       if (s < nf) {
         for (int j = 0; j < k; j++) fsrc.push_back(obj + (s * k + j) * M);
         for (int i = 0; i < p; i++) fdst.push_back(par + i * M);
+        if (want_fused) {
+          for (int j = 0; j < k; j++) q_src.push_back(obj + (s * k + j) * M);
+          for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
+          q_len.push_back(M);
+          q_dig.push_back(dig);
+        }
         if (dig) {
           for (int j = 0; j < k; j++) items.push_back({obj + (s * k + j) * M, M, dig + j * 16});
           for (int i = 0; i < p; i++) items.push_back({par + i * M, M, dig + (k + i) * 16});
@@ -988,6 +1003,12 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
         if (dig) {
           for (int j = 0; j < k; j++) ritems.push_back({td + j * cls, cl, dig + j * 16});
           for (int i = 0; i < p; i++) ritems.push_back({par + i * M, cl, dig + (k + i) * 16});
+        }
+        if (want_fused) {
+          for (int j = 0; j < k; j++) q_src.push_back(td + j * cls);
+          for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
+          q_len.push_back(cl);
+          q_dig.push_back(dig);
         }
         toff += k * cls;
       }
@@ -1015,11 +1036,36 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
       uprefix.push_back(uprefix.back() + (M + 15) / 16);
     }
   }
+  // fused: requests longest first (a workgroup's first request sets its steps)
+  const bool fused = want_fused && full_aligned && !q_len.empty();
+  std::vector<const uint8_t *> f_src;
+  std::vector<uint8_t *> f_dst, f_dig;
+  std::vector<int64_t> f_len;
+  if (fused) {
+    const size_t R = q_len.size();
+    std::vector<size_t> order(R);
+    for (size_t i = 0; i < R; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return q_len[x] > q_len[y]; });
+    f_src.reserve(R * k);
+    f_dst.reserve(R * p);
+    for (size_t o : order) {
+      f_src.insert(f_src.end(), q_src.begin() + o * k, q_src.begin() + (o + 1) * k);
+      f_dst.insert(f_dst.end(), q_dst.begin() + o * p, q_dst.begin() + (o + 1) * p);
+      f_len.push_back(q_len[o]);
+      f_dig.push_back(q_dig[o]);
+    }
+  }
+  const std::vector<uint8_t> scratch_pad(fused ? 4096 : 0, 0);  // idle lanes' device line
   struct Tab {
     const void *h;
     size_t bytes;
   };
-  const Tab tabs[] = {{fsrc.data(), fsrc.size() * sizeof(void *)},
+  const Tab tabs[] = {{f_src.data(), f_src.size() * sizeof(void *)},
+                      {f_dst.data(), f_dst.size() * sizeof(void *)},
+                      {f_len.data(), f_len.size() * sizeof(int64_t)},
+                      {f_dig.data(), f_dig.size() * sizeof(void *)},
+                      {scratch_pad.data(), scratch_pad.size()},
+                      {fsrc.data(), fsrc.size() * sizeof(void *)},
                       {fdst.data(), fdst.size() * sizeof(void *)},
                       {pads.data(), pads.size() * sizeof(PadChunks)},
                       {pad_bstart.data(), pad_bstart.size() * sizeof(uint32_t)},
@@ -1040,7 +1086,28 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   for (int i = 0; i < kTabs && !rc; i++)
     if (tabs[i].bytes) std::memcpy(slot->h + off[i], tabs[i].h, tabs[i].bytes);
   if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[kTabs], hipMemcpyHostToDevice, st), "tables H2D");
-  auto dptr = [&](int i) { return slot->d + off[i]; };
+  const int T0 = 5;  // the first five tables belong to the fused launch
+  auto dptr = [&](int i) { return slot->d + off[i + T0]; };
+  if (fused) {
+    if (!rc)
+      rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
+                             int64_t(pads.size()), pad_blocks, st);
+    FilesMd5Args fa;
+    std::memset(&fa, 0, sizeof(fa));
+    fa.src_ptrs = reinterpret_cast<const uint8_t *const *>(slot->d + off[0]);
+    fa.dst_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[1]);
+    fa.lens = reinterpret_cast<const int64_t *>(slot->d + off[2]);
+    fa.dig_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[3]);
+    fa.scratch = slot->d + off[4];
+    fa.nstripes = int64_t(f_len.size());
+    fa.k = k;
+    fa.p = p;
+    std::memcpy(fa.coef, prow, size_t(p) * k);
+    if (!rc) rc = launch_files_md5(fa, ctx->num_cus, st);
+    const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
+    release_slot(ctx, slot);
+    return rc ? rc : rc2;
+  }
   if (!rc && p > 0 && full_aligned && nfs > 0)
     rc = stripes_mul_impl(ctx, p, k, prow, nullptr, reinterpret_cast<const unsigned char *const *>(dptr(0)), nullptr,
                           0, 0, nullptr, reinterpret_cast<unsigned char *const *>(dptr(1)), nullptr, 0, 0, nullptr, M,

@@ -670,13 +670,16 @@ def test_survey_named_encode_entry_points(gpu_ctx):
     pb.free()
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("misalign,n,k,M", [(0, 9, 6, 4096), (3, 9, 6, 4096), (0, 9, 6, 1000), (0, 14, 10, 65536),
                                              (5, 14, 10, 16400), (0, 24, 20, 4096), (0, 6, 6, 4096)])
-def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
+def test_encode_objects_matches_per_object(gpu_ctx, monkeypatch, fused, misalign, n, k, M):
     """Many objects per call (full stripes in one gather launch, last stripes in
     one ragged work-queue launch -- the list kernel for k > 19 --, MD5 of every
     chunk in one list launch) equals encoding each object on its own with
-    nxec_encode_object; the tail arena holds the zero-padded last-stripe chunks."""
+    nxec_encode_object; the tail arena holds the zero-padded last-stripe chunks.
+    fused = "1": aligned batches with k <= 16 run as one k_files_md5 launch."""
+    monkeypatch.setenv("NXEC_FUSED_MD5", fused)
     p = n - k
     lengths = [0, 1, 17, k * M - 1, k * M, 3 * k * M + 100, 5000, 2 * k * M, 12345]
     total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
@@ -1199,3 +1202,52 @@ def test_config1_both_readings_golden(gpu_ctx, golden, n, k, cs):
         ob.free()
     obj.free()
     par.free()
+
+
+@pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (20, 16, 8192), (6, 4, 4096), (5, 1, 1024)])
+def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, k, M):
+    """Hundreds of files of random sizes (1 B .. 3 full stripes): the one-launch
+    multi-file write (k_files_md5, requests sorted longest first, per-request
+    lengths) gives the same parity, tail arena and digests as the separate
+    gather / pad / ragged / MD5-list launches, and the digests match hashlib."""
+    import hashlib
+    p = n - k
+    rng = np.random.default_rng(n * 1000 + M)
+    lengths = [int(x) for x in rng.integers(1, 3 * k * M + 1, size=300)] + [k * M, 1, 16, 17, k * M + 1]
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    offs, pos = [], 0
+    for L in lengths:
+        offs.append(pos)
+        pos += (L + 15) // 16 * 16
+    host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
+    arena = up(host)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NXEC_FUSED_MD5", mode)
+        par = nxec.DeviceBuffer(total * p * M)
+        par.memset(0)
+        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+        md5 = nxec.DeviceBuffer(total * n * 16)
+        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
+        out[mode] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
+        for b in (par, tail, md5):
+            b.free()
+    (p1, t1, m1), (p0, t0, m0) = out["1"], out["0"]
+    assert np.array_equal(t1, t0)
+    assert np.array_equal(m1, m0)
+    g = 0
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        for s in range(ns):
+            cs = M if s < nf else cl
+            assert np.array_equal(p1[g + s, :, :cs], p0[g + s, :, :cs]), (i, s)
+        g += ns
+    # spot-check digests against hashlib: a full stripe's data chunk and a last stripe's parity
+    i = next(j for j, L in enumerate(lengths) if L > k * M)
+    first = sum(nxec.object_layout(n, k, L, M)[0] for L in lengths[:i])
+    assert m1[first, 0].tobytes().hex() == hashlib.md5(host[offs[i]:offs[i] + M].tobytes()).hexdigest()
+    ns, nf, cl = nxec.object_layout(n, k, lengths[i], M)
+    if ns > nf and p > 0:
+        last = first + ns - 1
+        assert m1[last, k].tobytes().hex() == hashlib.md5(p1[last, 0, :cl].tobytes()).hexdigest()
+    arena.free()
