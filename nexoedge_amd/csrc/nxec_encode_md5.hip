@@ -390,7 +390,7 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
 // loads cross PCIe (microseconds each), so small k keeps more steps ahead
 template <int K>
 constexpr int gm_depth() {
-  return (200 - 2 * K) / (16 * K) >= 8 ? 8 : (200 - 2 * K) / (16 * K) < 2 ? 2 : (200 - 2 * K) / (16 * K);
+  return (200 - 2 * K) / (4 * K) >= 8 ? 8 : (200 - 2 * K) / (4 * K) < 2 ? 2 : (200 - 2 * K) / (4 * K);
 }
 
 // The agent's requests (container_manager.cc:221-258 partial encodes and
