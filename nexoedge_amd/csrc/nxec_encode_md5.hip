@@ -545,10 +545,11 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 }
 
 // Hash waves of k_files_md5: hash_rows with a length per lane.  Lane h's
-// chunk has my_steps steps, the last holding my_tail bytes (1..256; the row is
-// zero past them); the workgroup runs nsteps >= my_steps steps (its longest
-// request), and a lane that is done only keeps the barriers.  st comes back
-// finished (RFC 1321 padding built in registers).
+// chunk has my_steps steps, the last holding my_tail bytes (1..256; the row's
+// bytes past them are masked off here, so the code lanes need not zero them);
+// the workgroup runs nsteps >= my_steps steps (its longest request), and a
+// lane that is done only keeps the barriers.  st comes back finished (RFC
+// 1321 padding built in registers).
 __device__ __forceinline__ void hash_rows_var(const uint8_t *buf, uint32_t buf_bytes, int h, bool active, int nsteps,
                                               int my_steps, int my_tail, uint64_t len, uint32_t (&st)[4]) {
   const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
@@ -582,7 +583,10 @@ __device__ __forceinline__ void hash_rows_var(const uint8_t *buf, uint32_t buf_b
 #pragma unroll
       for (int b = 0; b < kEncMd5Step / 64; b++)
         if (b == fb) x = m[16 * b + i];
-      w[i] = x | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
+      // keep the word's bytes below r, then the 0x80 terminator
+      const int keep = r - 4 * i;  // bytes of this word inside the chunk
+      const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+      w[i] = (x & mask) | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
     }
     const uint32_t lo = static_cast<uint32_t>(len * 8), hi = static_cast<uint32_t>((len * 8) >> 32);
     if (r >= 56) {
@@ -624,7 +628,8 @@ __device__ __forceinline__ void hash_rows_var(const uint8_t *buf, uint32_t buf_b
 // zero-padded last stripe in the tail arena) with its own chunk length.
 // Requests come sorted longest first, so a workgroup's first request sets its
 // step count; a lane past its request's end re-reads its last in-bounds
-// vector, stores to scratch and leaves zeros in its LDS row.
+// vector, stores to scratch and leaves its LDS row alone (the hash lanes mask
+// the bytes past a chunk's end).
 template <int K>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
@@ -660,7 +665,6 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     for (int r = 0; r < kMaxRowsPerPass; r++)
       dp[r] = tmax >= 0 && r < a.p ? a.dst_ptrs[sx * a.p + r] + v * 16 : a.scratch + 256 * (r + 1) + v * 16;
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
-    const u32x4 zero{0u, 0u, 0u, 0u};
     auto load = [&](int step, u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(step, tcl)) * kEncMd5Step;
 #pragma unroll
@@ -674,9 +678,9 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int i = 0; i < 16; i++) acc[i] = 0;
 #pragma unroll
       for (int j = 0; j < K; j += 2) {
-        if (act) {
-          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = ok ? d[j] : zero;
-          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = ok ? d[j + 1] : zero;
+        if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
+          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
         }
         lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
 #pragma unroll
@@ -690,7 +694,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
           dev::st_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
-          if (act) *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = ok ? pv : zero;
+          if (ok) *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = pv;
         }
       }
       lds_barrier();
