@@ -1204,7 +1204,8 @@ def test_config1_both_readings_golden(gpu_ctx, golden, n, k, cs):
     par.free()
 
 
-@pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (20, 16, 8192), (6, 4, 4096), (5, 1, 1024)])
+@pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (20, 16, 8192), (6, 4, 4096), (5, 1, 1024), (9, 6, 4112),
+                                   (7, 3, 208)])
 def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, k, M):
     """Hundreds of files of random sizes (1 B .. 3 full stripes): the one-launch
     multi-file write (k_files_md5, requests sorted longest first, per-request
