@@ -1337,9 +1337,17 @@ static int agent_slot(nxec_ctx_t *ctx, AgentBatch &b, size_t bytes) {
 // MD5 chain (~9 ms per 1 MiB chunk whatever its size), so requests in mapped
 // buffers all go in one launch (64 MiB staging batches: 23 -> 11 GiB/s at one
 // caller).  Slots rotate with the two-kernel form's.
+// md5 = false (a group that wants no digests: ENC_CHUNK_REQ, whose
+// getEncodedChunks computes none, container_manager.cc:221-258): when every
+// input is mapped the same tables feed the gather form of the multiply
+// kernel -- zero copy, no MD5 chain (64 x 4->1 arena requests: 1 caller 37 ->
+// 50 GiB/s); with inputs to stage, *taken = false and the caller runs the
+// H2D -> multiply -> D2H form, whose copy engines beat kernel reads of the
+// staging slot when no MD5 chain hides them (pageable: 34 vs 29 GiB/s).
 static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const std::vector<int> &ids,
                              int64_t chunk_size, int64_t stride, int64_t batch_bytes, AgentBatch (&slots)[kAgentSlots],
-                             int &cur) {
+                             int &cur, bool md5, bool *taken) {
+  *taken = true;
   const nxec_agent_req &r0 = reqs[ids[0]];
   const int ni = r0.ninputs, no = r0.noutputs;
   const size_t nid = ids.size(), cs = size_t(chunk_size);
@@ -1359,6 +1367,10 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
   if (agent_trace())
     std::fprintf(stderr, "agent fused group of %zu: classify %zu buffers %.3f ms\n", nid, nid * (ni + no),
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
+  if (!md5 && std::find(in_dv.begin(), in_dv.end(), uintptr_t(0)) != in_dv.end()) {
+    *taken = false;
+    return NXEC_OK;
+  }
   int rc = NXEC_OK;
   for (size_t first = 0; first < nid && rc == NXEC_OK;) {
     // [first, last): requests whose staging fits batch_bytes (at least one)
@@ -1368,7 +1380,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       int64_t n_st = 0;
       for (int j = 0; j < ni; j++) n_st += in_dv[last * ni + j] == 0;
       for (int o = 0; o < no; o++) n_st += out_dv[last * no + o] == 0;
-      const int64_t need = n_st * stride + int64_t(no) * 16 + (int64_t(ni) + no) * 8;
+      const int64_t need = n_st * stride + (md5 ? int64_t(no) * 16 : 0) + (int64_t(ni) + no) * 8;
       if (last > first && staged + need > batch_bytes) break;
       staged += need;
       last++;
@@ -1396,7 +1408,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
     b.fused = true;
     b.stride = stride;
     b.md5_off = size_t(pos);
-    const size_t tab_off = b.md5_off + nb * no * 16;
+    const size_t tab_off = b.md5_off + (md5 ? nb * no * 16 : 0);
     uint64_t *src_tab = reinterpret_cast<uint64_t *>(b.slot->h + tab_off);
     uint64_t *dst_tab = src_tab + nb * ni;
     HostPool::get().parallel_for(static_cast<int>(nb * (ni + no)), [&](int item) {
@@ -1419,6 +1431,17 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       std::fprintf(stderr, "agent fused batch of %zu (%lld staged bytes): finish-previous %.2f ms, tables + gather %.2f ms\n",
                    nb, static_cast<long long>(pos), std::chrono::duration<double, std::milli>(tr1 - tr0).count(),
                    std::chrono::duration<double, std::milli>(tr2 - tr1).count());
+    }
+    if (!md5) {  // CodingUtils::encode of the batch over the pointer tables
+      rc = stripes_mul_impl(ctx, no, ni, r0.matrix, nullptr,
+                            reinterpret_cast<const unsigned char *const *>(hv + tab_off), nullptr, 0, 0, nullptr,
+                            reinterpret_cast<unsigned char *const *>(hv + tab_off + nb * ni * 8), nullptr, 0, 0,
+                            nullptr, chunk_size, int64_t(nb), b.slot->stream);
+      if (rc) break;
+      b.d2h_bytes = 0;
+      rc = agent_d2h(ctx, other);
+      first = last;
+      continue;
     }
     GatherMd5Args ga;
     std::memset(&ga, 0, sizeof(ga));
@@ -1478,9 +1501,11 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     const int ni = r0.ninputs, no = r0.noutputs;
     bool group_md5 = false;
     for (int id : ids) group_md5 |= reqs[id].md5 != nullptr;
-    if (fused_env && host_direct && group_md5 && ni <= kGatherMd5MaxK && no <= kMaxRowsPerPass) {
-      if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur))) break;
-      continue;
+    if (fused_env && host_direct && ni <= kGatherMd5MaxK && no <= kMaxRowsPerPass) {
+      bool taken = false;
+      if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur, group_md5, &taken)))
+        break;
+      if (taken) continue;
     }
     const int64_t per = (int64_t(ni) + no) * stride + int64_t(no) * 16;
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));

@@ -145,7 +145,11 @@ def test_agent_fused_any_chunk_size(gpu_ctx, cs):
 
 
 @pytest.mark.gpu
-def test_agent_without_digests_keeps_two_kernel_form(gpu_ctx):
-    """A group that asks for no digest at all runs H2D -> multiply -> D2H."""
-    run_batch(gpu_ctx, [(4, 1)], 65536, "arena", "arena", nreq=6, seed=6, with_md5=lambda r: False)
-    run_batch(gpu_ctx, [(4, 1), (12, 2)], 65536 + 16, "arena", "pageable", nreq=6, seed=5, with_md5=lambda r: False)
+@pytest.mark.parametrize("in_kind,out_kind", [("arena", "arena"), ("pageable", "pageable"), ("mixed", "mixed"),
+                                              ("misaligned", "arena")])
+@pytest.mark.parametrize("cs", [65536, 65536 + 16, 5000, 1])
+def test_agent_without_digests_zero_copy(gpu_ctx, in_kind, out_kind, cs):
+    """Groups that want no digest (ENC_CHUNK_REQ: getEncodedChunks computes
+    none) run the gather form of the multiply kernel over the same pointer
+    tables -- mapped buffers in place, the others through the slot."""
+    run_batch(gpu_ctx, SHAPES, cs, in_kind, out_kind, nreq=10, seed=cs + 7, with_md5=lambda r: False)

@@ -101,6 +101,9 @@ int main(int argc, char **argv) {
       const uint8_t row[4] = {0x1d, 0x3a, 0x74, 0xe8};
       std::vector<int> tlist{1, 4, 16};
       if (const char *e = std::getenv("DROPIN_AGENT_THREADS")) tlist = {std::atoi(e)};
+      // DROPIN_AGENT_MD5=0: ENC_CHUNK_REQ-shaped requests (getEncodedChunks computes no digest)
+      const char *me = std::getenv("DROPIN_AGENT_MD5");
+      const bool with_md5 = !(me && me[0] == '0');
       // chunk buffers: pageable (the reference's containers malloc them,
       // fs.cc:180) or arena blocks (an agent whose container reads land in
       // Chunk::allocateData buffers): the fused kernel then reads and writes
@@ -137,7 +140,7 @@ int main(int argc, char **argv) {
             for (int r = 0; r < nreq; r++) {
               for (int j = 0; j < ni; j++) ip[r * ni + j] = in + (static_cast<size_t>(r) * ni + j) * cs;
               op[r] = out + static_cast<size_t>(r) * cs;
-              reqs[r] = {ni, 1, row, ip.data() + r * ni, op.data() + r, md5.data() + r * 16};
+              reqs[r] = {ni, 1, row, ip.data() + r * ni, op.data() + r, with_md5 ? md5.data() + r * 16 : nullptr};
             }
             while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < secs) {
               if (nxec_agent_encode_batch(ctx, reqs.data(), nreq, cs, 0) != NXEC_OK) ok = false;
@@ -151,10 +154,10 @@ int main(int argc, char **argv) {
         for (auto &th : pool) th.join();
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         const double bytes = static_cast<double>(calls) * nreq * (ni + 1) * cs;
-        std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes + MD5)\", \"buffers\": \"%s\", "
+        std::printf("{\"path\": \"nxec_agent_encode_batch (64 x 4->1 partial encodes%s)\", \"buffers\": \"%s\", "
                     "\"threads\": %d, \"chunk\": %d, \"calls\": %ld, \"GiB_s\": %.2f, \"ms_per_call\": %.3f, "
                     "\"ok\": %s}\n",
-                    arena ? "arena" : "pageable", threads, cs, static_cast<long>(calls), bytes / dt / (1 << 30),
+                    with_md5 ? " + MD5" : "", arena ? "arena" : "pageable", threads, cs, static_cast<long>(calls), bytes / dt / (1 << 30),
                     1e3 * dt * threads / static_cast<double>(calls), ok ? "true" : "false");
         std::fflush(stdout);
       }
