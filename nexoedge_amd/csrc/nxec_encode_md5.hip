@@ -668,7 +668,16 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     auto load = [&](int step, u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(step, tcl)) * kEncMd5Step;
 #pragma unroll
-      for (int j = 0; j < K; j++) d[j] = dev::ld_stream(sp[j] + off);
+      for (int j = 0; j < K; j++) {
+        // plain (cached) loads: a chunk that is not 128-byte aligned (a tail
+        // arena chunk at a 16-byte stride, an object at any 16-byte offset)
+        // shares its boundary lines between consecutive steps; streaming
+        // loads fetched them once per step
+        if (a.cached_loads)
+          d[j] = *reinterpret_cast<const u32x4 *>(sp[j] + off);
+        else
+          d[j] = dev::ld_stream(sp[j] + off);
+      }
     };
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = step <= tmax;
@@ -849,6 +858,8 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
       !in.lens || !in.dig_ptrs || !in.scratch)
     return set_error(NXEC_ERR_INVALID, "files+md5: unsupported arguments");
   FilesMd5Args a = in;
+  a.cached_loads = 1;  // FETCH x2 60.0 -> 43.6 GB per 4096-file batch (= the data bytes), same time
+  if (const char *e = std::getenv("NXEC_FILES_LOADS")) a.cached_loads = e[0] != '0';
   const int nh = a.k + a.p;
   int64_t S = std::min(kEmMaxStripes, kEmMaxRows / nh);
   const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);

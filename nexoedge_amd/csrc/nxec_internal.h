@@ -228,6 +228,7 @@ struct FilesMd5Args {
   int64_t nstripes;
   int32_t k, p;
   int32_t stripes_per_group;  // set by launch_files_md5
+  int32_t cached_loads;       // plain loads (default); NXEC_FILES_LOADS=0 streaming (A/B)
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
 };
 int launch_files_md5(const FilesMd5Args &a, int num_cus, void *stream);
