@@ -12,13 +12,13 @@ CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip \
-            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_config.cpp \
+            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_device.h $(wildcard $(CSRC)/coding/*.hh)
 
 all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test \
-     build/stripe_batch_test
+     build/stripe_batch_test build/chunk_replay_test
 
 # rs.cc's ISA-L call sequence compiled against include/nxec_isal_compat.h (plain C)
 build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h $(LIBDIR)/libnxec.so
@@ -32,6 +32,11 @@ build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 
 # batched ChunkManager entry vs the per-stripe RSCode path
 build/stripe_batch_test: tests/cpp/stripe_batch_test.cc $(LIBDIR)/libnxec.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
+
+# the reference's Chunk ownership sequences (shallow copies + freeData = false)
+build/chunk_replay_test: tests/cpp/chunk_replay_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
 
@@ -97,13 +102,17 @@ build/san/$(1)/libnxec.so: $(patsubst $(CSRC)/%,build/san/$(1)/obj/%.o,$(SAN_SRC
 build/san/$(1)/host_sanity_test: tests/cpp/host_sanity_test.cc build/san/$(1)/libnxec.so $(HDRS)
 	$(HIPCC) -O1 -g $(CXXSTD) $(2) -Iinclude -I$(CSRC) $$< -Lbuild/san/$(1) -lnxec \
 	    -Wl,-rpath,'$$$$ORIGIN' -lcrypto -lpthread -o $$@
-$(1): build/san/$(1)/host_sanity_test
+build/san/$(1)/chunk_replay_test: tests/cpp/chunk_replay_test.cc build/san/$(1)/libnxec.so $(HDRS)
+	$(HIPCC) -O1 -g $(CXXSTD) $(2) -Iinclude -I$(CSRC) $$< -Lbuild/san/$(1) -lnxec \
+	    -Wl,-rpath,'$$$$ORIGIN' -lcrypto -lpthread -o $$@
+$(1): build/san/$(1)/host_sanity_test build/san/$(1)/chunk_replay_test
 endef
 $(eval $(call SAN_RULES,asan,$(SAN_ASAN)))
 $(eval $(call SAN_RULES,ubsan,$(SAN_UBSAN)))
 $(eval $(call SAN_RULES,tsan,$(SAN_TSAN)))
 sanitize: asan ubsan tsan
 	ASAN_OPTIONS=detect_leaks=1 LSAN_OPTIONS=suppressions=tests/cpp/lsan.supp build/san/asan/host_sanity_test
+	ASAN_OPTIONS=detect_leaks=1 LSAN_OPTIONS=suppressions=tests/cpp/lsan.supp build/san/asan/chunk_replay_test
 	UBSAN_OPTIONS=print_stacktrace=1 build/san/ubsan/host_sanity_test
 	TSAN_OPTIONS=ignore_noninstrumented_modules=1 build/san/tsan/host_sanity_test
 

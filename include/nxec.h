@@ -492,6 +492,32 @@ int nxec_host_arena_stats(size_t *pinned_bytes, size_t *in_use_bytes);
 int nxec_host_range_mapped(const void *p, size_t bytes);
 
 /* ---------------------------------------------------------------------------
+ * 6b. Digests computed by a coding pass, for Chunk::computeMD5 (reference
+ *     chunk.hh:136-143).  The reference hashes the chunks it has just coded
+ *     right after the coding call on the same thread (chunk_manager.cc:99 ->
+ *     :175, :1141 -> :1173, agent.cc:339 -> :342); RSCode::encode (every
+ *     chunk, marked on the Chunk itself) and RSCode::decode(isRepair) (the
+ *     repaired regions) hash them in the same GPU kernel instead, and the
+ *     regions' digests wait here, per calling thread, keyed by (pointer,
+ *     length).  Each noting call clears the thread's table first; an entry is
+ *     taken once; Chunk::release forgets its buffer's entry.
+ *     nxec_chunk_md5_mode: NXEC_CHUNK_MD5 = 0 (never; computeMD5 hashes on the
+ *     host), 1 (default: RSCode::encode, whose n digests per stripe the GPU
+ *     finishes sooner than one host thread hashing them in turn), 2 (also the
+ *     repaired chunks of RSCode::decode(isRepair) and the outputs of
+ *     CodingUtils::encode -- the agent's RPR_CHUNK_REQ hashes them,
+ *     agent.cc:342, its ENC_CHUNK_REQ does not, container_manager.cc:251;
+ *     one to four chunks per call, so a GPU hash chain (~10 ms per MiB on one
+ *     lane) only pays with many concurrent callers).
+ * ------------------------------------------------------------------------- */
+int nxec_chunk_md5_mode(void);
+void nxec_digest_clear(void);
+int nxec_digest_note(const void *p, int64_t len, const unsigned char *md5);
+/* 1 and the digest in md5[16] if (p, len) was noted on this thread (the entry is removed), else 0 */
+int nxec_digest_take(const void *p, int64_t len, unsigned char *md5);
+void nxec_digest_forget(const void *p);
+
+/* ---------------------------------------------------------------------------
  * 7. Recovery and testing hooks.
  * ------------------------------------------------------------------------- */
 /* Zero every work-queue slot of the calling thread's current device

@@ -112,6 +112,11 @@ _PROTOS = {
     "nxec_host_arena_owns": (C.c_int, [vp]),
     "nxec_host_arena_stats": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "nxec_host_range_mapped": (C.c_int, [vp, C.c_size_t]),
+    "nxec_chunk_md5_mode": (C.c_int, []),
+    "nxec_digest_clear": (None, []),
+    "nxec_digest_note": (C.c_int, [vp, i64, vp]),
+    "nxec_digest_take": (C.c_int, [vp, i64, vp]),
+    "nxec_digest_forget": (None, [vp]),
     "nxec_storage_classes_load": (C.c_int, [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]),
     "nxec_proxy_repair_using_car": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
     "nxec_reset_work_queues": (C.c_int, []),

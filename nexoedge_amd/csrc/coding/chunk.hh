@@ -2,15 +2,39 @@
 // src/ds/chunk.hh:15-186) -- the same fields, methods and ownership rules, so
 // proxy and agent code written against the reference compiles unchanged.
 //
-// One difference, the reason this header exists: allocateData takes buffers
-// of 64 KiB and more from libnxec's pinned host arena (nxec_host_alloc,
-// include/nxec.h §6) instead of posix_memalign/malloc.  They are page
-// aligned (>= the 32 bytes chunk.hh:66 asks for) and device-mapped, so
-// RSCode::encode / CodingUtils::encode give them to the GPU without a staging
-// copy.  release() returns arena buffers to the arena and free()s everything
-// else, so buffers the caller malloc()ed and attached (io.cc:213,
-// container_manager.cc:241) keep working.  Without a usable GPU, or past the
-// arena's bound, allocation falls back to ordinary memory.
+// Copy semantics are the reference's: Chunk declares no copy or move
+// operators, so `a = b` and pass-by-value are the implicit memberwise
+// (shallow) copy that aliases b's buffer.  The reference relies on it --
+// `events[i].chunks[j] = file.chunks[idx]; events[i].chunks[j].freeData =
+// false;` (chunk_manager.cc:176-178, :1275-1276, :1498-1499,
+// proxy_file_ops.cc:585-586, agent.cc:366-367) hands a borrowed view of the
+// same bytes to the send path -- and copy() / move() stay the explicit deep
+// copy and ownership transfer.  As in the reference, a std::vector<Chunk>
+// that owns buffers must not reallocate (resize first, then move() in place,
+// chunk_manager.cc:765-775, :1129-1132).
+//
+// Two differences, the reasons this header exists:
+//  * allocateData takes buffers of 64 KiB and more from libnxec's pinned host
+//    arena (nxec_host_alloc, include/nxec.h §6) instead of
+//    posix_memalign/malloc.  They are page aligned (>= the 32 bytes
+//    chunk.hh:66 asks for) and device-mapped, so RSCode::encode /
+//    CodingUtils::encode give them to the GPU without a staging copy.
+//    release() returns arena buffers to the arena and free()s everything
+//    else, so buffers the caller malloc()ed and attached (io.cc:213,
+//    container_manager.cc:241) keep working.  Without a usable GPU, or past
+//    the arena's bound, allocation falls back to ordinary memory.
+//  * computeMD5 may return a digest the GPU computed in the coding pass that
+//    produced the bytes (include/nxec.h §6b): RSCode::encode hashes all n
+//    chunks of the stripe in its kernel and marks each chunk's digest valid
+//    for exactly (data, size); RSCode::decode(isRepair) and, on request,
+//    CodingUtils::encode leave their outputs' digests in a per-thread table
+//    keyed by (pointer, length).  A marked digest is used once and only while
+//    the buffer is the one it was computed for: allocateData, copy, move (of
+//    the destination), release and reset drop the mark, and copyMeta never
+//    carries it.  The reference's sequences between the coding call and the
+//    hash write nothing to the chunks (chunk_manager.cc:99 -> :175,
+//    :1141 -> :1173, agent.cc:339 -> :342).  NXEC_CHUNK_MD5=0 disables the
+//    cached digests; verifyMD5 always hashes.
 //
 // File uuids are boost::uuids::uuid when boost is available (the Nexoedge
 // build), else a 16-byte value type of the same layout.
@@ -75,27 +99,13 @@ struct Chunk {
   int fileVersion;                           /**< file version number */
   char chunkVersion[CHUNK_VERSION_MAX_LEN];  /**< chunk version number for revert */
   unsigned char md5[MD5_DIGEST_LENGTH];      /**< chunk md5 checksum */
+  // md5 holds the digest the GPU computed for exactly these bytes: valid
+  // while data == digestData and size == digestSize (not in the reference)
+  const unsigned char *digestData;
+  int digestSize;
 
   Chunk() { reset(); }
   ~Chunk() { release(); }
-  // copies are deep and moves transfer the buffer (the reference's explicit
-  // copy() / move() semantics), so std::vector<Chunk> never double-frees
-  Chunk(const Chunk &o) {
-    reset();
-    copy(o);
-  }
-  Chunk &operator=(const Chunk &o) {
-    if (this != &o) copy(o);
-    return *this;
-  }
-  Chunk(Chunk &&o) noexcept {
-    reset();
-    move(o);
-  }
-  Chunk &operator=(Chunk &&o) noexcept {
-    if (this != &o) move(o);
-    return *this;
-  }
 
   void copyMeta(const Chunk &src, bool copySize = true) {
     setId(src.namespaceId, src.fuuid, src.chunkId);
@@ -116,6 +126,7 @@ struct Chunk {
   // same size unless alignment is requested
   bool allocateData(int sizet, bool aligned = false) {
     if (sizet <= 0) return false;
+    dropDigest();  // the caller is about to (re)write the bytes
     if (data != NULL && size == sizet && freeData && !aligned) return true;
     unsigned char *datat = NULL;
     const size_t min = chunk_arena_min_bytes();
@@ -138,22 +149,29 @@ struct Chunk {
     return true;
   }
 
+  // chunk.hh:87-95; a metadata-only source (no buffer) copies its metadata
+  // and leaves this chunk without a buffer instead of reading NULL
   bool copy(const Chunk &src, bool aligned = false) {
     release();
     copyMeta(src);
+    if (src.data == NULL && src.size > 0) return true;
     if (!allocateData(src.size, aligned)) return false;
     memcpy(data, src.data, size);
     return true;
   }
 
+  // chunk.hh:97-106; a digest computed for the buffer travels with it
   bool move(Chunk &src) {
     release();
     copyMeta(src);
     data = src.data;
     size = src.size;
     freeData = src.freeData;
+    digestData = src.digestData;
+    digestSize = src.digestSize;
     src.data = 0;
     src.freeData = false;
+    src.dropDigest();
     return true;
   }
 
@@ -168,9 +186,18 @@ struct Chunk {
            std::to_string(chunkId);
   }
 
-  // chunk.hh:136-152 (OpenSSL MD5, as MD5Calculator does)
+  // chunk.hh:136-143 (OpenSSL MD5, as MD5Calculator does), or the digest the
+  // coding pass that wrote these bytes computed on the GPU (see the top)
   bool computeMD5() {
     if (size <= 0) return false;
+    if (data != NULL && nxec_chunk_md5_mode() > 0) {
+      if (digestData == data && digestSize == size) {
+        dropDigest();  // used once
+        return true;
+      }
+      if (nxec_digest_take(data, size, md5) == 1) return true;
+    }
+    dropDigest();
     unsigned int len = MD5_DIGEST_LENGTH;
     return EVP_Digest(data, static_cast<size_t>(size), md5, &len, EVP_md5(), NULL) == 1;
   }
@@ -181,6 +208,16 @@ struct Chunk {
     return memcmp(md5, cur, MD5_DIGEST_LENGTH) == 0;
   }
   void copyMD5(const Chunk &src) { memcpy(md5, src.md5, MD5_DIGEST_LENGTH); }
+
+  // marks md5 (already filled) as the digest of the current buffer
+  void setDigestValid() {
+    digestData = data;
+    digestSize = size;
+  }
+  void dropDigest() {
+    digestData = NULL;
+    digestSize = 0;
+  }
 
   // chunk.hh:158-164, kept as is (including its memcmp truthiness)
   bool matchMeta(const Chunk &in) {
@@ -198,6 +235,7 @@ struct Chunk {
     size = 0;
     freeData = true;
     resetMD5();
+    dropDigest();
   }
 
   void release() {
@@ -207,6 +245,7 @@ struct Chunk {
 
   static void freeBuffer(unsigned char *p) {
     if (!p) return;
+    nxec_digest_forget(p);
     if (nxec_host_arena_owns(p)) nxec_host_free(p);
     else free(p);
   }

@@ -52,16 +52,17 @@ static std::string sha(const uint8_t *p, size_t n) {
 }
 
 // ContainerManager::getEncodedChunks (container_manager.cc:221-258): the
-// agent's partial encode of its local chunks with its slice of the submatrix
-static Chunk agentEncode(std::vector<Chunk> &stripe, const int *cids, int numChunks, unsigned char *matrix) {
-  Chunk coded;
+// agent's partial encode of its local chunks with its slice of the submatrix,
+// into `coded` (an element of a vector sized beforehand: Chunk copies are
+// shallow, as in the reference, so owners are filled in place, never copied)
+static void agentEncode(std::vector<Chunk> &stripe, const int *cids, int numChunks, unsigned char *matrix,
+                        Chunk &coded) {
   std::vector<unsigned char *> raw(numChunks);
   for (int i = 0; i < numChunks; i++) raw[i] = stripe.at(cids[i]).data;
   coded.data = static_cast<unsigned char *>(std::malloc(stripe.at(cids[0]).size));
   coded.size = stripe.at(cids[0]).size;
   if (!CodingUtils::encode(raw.data(), numChunks, &coded.data, 1, coded.size, matrix)) coded.size = 0;
   coded.freeData = true;
-  return coded;
 }
 
 static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bool atProxyCfg) {
@@ -158,6 +159,7 @@ static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bo
   bool ok = false;
   if (isRepairAtProxy) {
     std::vector<Chunk> inputChunks;
+    inputChunks.reserve(static_cast<size_t>(numInputChunks) + 1);
     if (isRepairUsingCAR) {
       // accessGroupedChunks (chunk_manager.cc:1683-1711): ENC_CHUNK_REQ per group,
       // coefficients = the next numChunks bytes of the submatrix
@@ -165,7 +167,8 @@ static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bo
         const int *grp = &subChunkGroups[i * (numInputChunks + 1)];
         std::vector<unsigned char> coef(submatrix.begin() + midx, submatrix.begin() + midx + grp[0]);
         midx += grp[0];
-        inputChunks.push_back(agentEncode(stripe, grp + 1, grp[0], coef.data()));
+        inputChunks.emplace_back();
+        agentEncode(stripe, grp + 1, grp[0], coef.data(), inputChunks.back());
         std::printf("PART %d %s\n", i, sha(inputChunks.back().data, cs).c_str());
       }
       numInputChunks = numSubChunkGroups;  // chunk_manager.cc:1034
@@ -188,6 +191,7 @@ static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bo
     if (!car) {
       // negative control: the same partials without CAR are refused (rs.cc:133-136)
       std::vector<Chunk> partials;
+      partials.reserve(2);
       for (int i = 0; i < 2 && i < k - 1; i++) {
         partials.emplace_back();
         partials.back().copy(stripe.at(i));
@@ -205,6 +209,7 @@ static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bo
                                                                           plan.getRepairMatrixSize());
     const int numReq = isRepairUsingCAR ? numSubChunkGroups : numInputChunks;
     std::vector<Chunk> replies;
+    replies.reserve(numReq);
     std::vector<unsigned char> matrix(numReq, 1);
     int cpos = 0;
     for (int i = 0; i < numReq; i++) {
@@ -212,8 +217,9 @@ static bool runCase(int n, int k, int cs, int failed, int rackSize, bool car, bo
         const int numChunks = subChunkGroups[i + cpos];
         std::vector<int> cids(numChunks);
         for (int j = 0; j < numChunks; j++) cids[j] = subChunkGroups[cpos + i + j + 1];
-        replies.push_back(
-            agentEncode(stripe, cids.data(), numChunks, reinterpret_cast<unsigned char *>(&codingState[cpos])));
+        replies.emplace_back();
+        agentEncode(stripe, cids.data(), numChunks, reinterpret_cast<unsigned char *>(&codingState[cpos]),
+                    replies.back());
         std::printf("PART %d %s\n", i, sha(replies.back().data, cs).c_str());
         cpos += numChunks;
       } else {

@@ -168,14 +168,46 @@ static void surface(int tid) {
   length_t osz = 0;
   CHECK(!code->decode(in, &out, osz, plan, nullptr), "insufficient inputs refused");
   CHECK(out == nullptr, "no buffer on refusal");
-  // Chunk ownership: copies are deep, moves transfer
+  // Chunk ownership as in the reference: copy() is deep, move() transfers,
+  // `=` is the implicit shallow copy that borrowers disown (freeData = false)
   Chunk c1;
   CHECK(c1.copy(in[0]) && c1.data != in[0].data && std::memcmp(c1.data, in[0].data, cs) == 0, "deep copy");
-  Chunk c2(std::move(c1));
+  Chunk c2;
+  c2.move(c1);
   CHECK(c1.data == nullptr && c2.size == cs, "move");
-  std::vector<Chunk> v;
-  for (int i = 0; i < 8; i++) v.push_back(c2);
+  {
+    std::vector<Chunk> v(8);
+    for (int i = 0; i < 8; i++) {
+      v[i] = c2;  // chunk_manager.cc:176-178
+      v[i].freeData = false;
+      CHECK(v[i].data == c2.data && v[i].size == c2.size, "shallow alias");
+    }
+  }
+  CHECK(c2.data != nullptr && c2.freeData, "owner intact after its borrowers died");
   CHECK(c2.computeMD5() && c2.verifyMD5(), "md5");
+  Chunk meta;  // metadata-only source: copy() must not read a NULL buffer
+  meta.setChunkId(3);
+  meta.size = cs;
+  Chunk c3;
+  CHECK(c3.copy(meta) && c3.data == nullptr && c3.size == cs && c3.chunkId == 3, "metadata-only copy");
+  // a digest noted for a buffer is taken once, by (pointer, length) only, on this thread
+  unsigned char dg[16], got[16];
+  for (int i = 0; i < 16; i++) dg[i] = static_cast<unsigned char>(tid * 16 + i);
+  nxec_digest_clear();
+  CHECK(nxec_digest_note(c2.data, cs, dg) == NXEC_OK, "note");
+  CHECK(nxec_digest_take(c2.data, cs - 1, got) == 0, "length must match");
+  CHECK(nxec_digest_note(c2.data, cs, dg) == NXEC_OK, "note again");
+  CHECK(nxec_digest_take(c2.data, cs, got) == 1 && std::memcmp(got, dg, 16) == 0, "take");
+  CHECK(nxec_digest_take(c2.data, cs, got) == 0, "taken once");
+  CHECK(nxec_digest_note(c2.data, cs, dg) == NXEC_OK, "note for computeMD5");
+  if (nxec_chunk_md5_mode() > 0) {
+    CHECK(c2.computeMD5() && std::memcmp(c2.md5, dg, 16) == 0, "computeMD5 returns the noted digest");
+    CHECK(c2.computeMD5() && c2.verifyMD5(), "then hashes again");
+  }
+  CHECK(nxec_digest_note(c2.data, cs, dg) == NXEC_OK, "note before release");
+  unsigned char *gone = c2.data;
+  c2.release();  // frees the buffer and forgets its digest
+  CHECK(nxec_digest_take(gone, cs, got) == 0, "forgotten on release");
   delete code;
 }
 

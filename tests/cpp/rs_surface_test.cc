@@ -144,6 +144,7 @@ static bool run(int n, int k, int cs, bool car) {
       data_t *rm = plan.getRepairMatrix();
       num_t cidx = 0;
       int inRack = 0;
+      rin.reserve(r);  // owners must not be moved by a reallocation (shallow Chunk copies)
       for (int cr = 0, rn = 0; cr < r && cidx < sel; cr++, rn += inRack) {
         inRack = n / r + (cr < n % r);
         const int rackEnd = rn + inRack;
@@ -160,7 +161,8 @@ static bool run(int n, int k, int cs, bool car) {
         unsigned char *pout[1] = {part.data};
         EXPECT(CodingUtils::encode(pin.data(), static_cast<int>(pin.size()), pout, 1, cs, rm + start),
                "partial encode");
-        rin.push_back(std::move(part));
+        rin.emplace_back();
+        rin.back().move(part);
       }
     }
     out = nullptr;

@@ -78,6 +78,7 @@ static void check_file(int n, int k, length_t M, uint64_t length) {
        {std::vector<chunk_id_t>{}, std::vector<chunk_id_t>{0}, std::vector<chunk_id_t>{1, static_cast<chunk_id_t>(n - 1)}}) {
     if (static_cast<int>(failed.size()) > n - k) continue;
     std::vector<Chunk> inputs;
+    inputs.reserve(ns * k);  // Chunk copies are shallow (as in the reference): never reallocate owners
     for (uint64_t s = 0; s < ns; s++) {
       int taken = 0;
       for (int i = 0; i < n && taken < k; i++) {
@@ -127,6 +128,7 @@ static void rate(uint64_t mib) {
     std::vector<chunk_id_t> failed{0, 1, 2, 3};
     std::vector<Chunk> inputs;
     const uint64_t ns = batch.numStripes(length, M);
+    inputs.reserve(ns * k);
     for (uint64_t s = 0; s < ns; s++)
       for (int i = 4; i < 4 + k; i++) {
         inputs.emplace_back();

@@ -170,3 +170,27 @@ def test_stripe_batch_matches_per_stripe_rscode():
     chunk of every stripe, plus OpenSSL MD5 and the decoded file."""
     r = subprocess.run([BATCH], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("PASSED 0 failures"), (r.stdout[-3000:], r.stderr[-2000:])
+
+
+REPLAY = os.path.join(ROOT, "build", "chunk_replay_test")
+
+
+def test_chunk_replay_cpu():
+    """The reference's Chunk ownership sequences (shallow `=` + freeData =
+    false, move, return by value) against csrc/coding/chunk.hh without a GPU:
+    every alias is the original buffer, every MD5 matches its bytes."""
+    assert os.path.exists(REPLAY), "run `make` (build/chunk_replay_test)"
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([REPLAY], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "PASSED 0 failures" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cs", ["262144", "1048576", "1000"])
+def test_chunk_replay_gpu(cs):
+    """The same sequences with RSCode::encode / CodingUtils::encode on the GPU:
+    writeFileStripe's computeMD5 (chunk_manager.cc:175) returns the digests the
+    encode kernel computed, and each equals OpenSSL's MD5 of the chunk's bytes
+    (checked in the binary for every chunk and every borrowed view)."""
+    r = subprocess.run([REPLAY, cs], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "PASSED 0 failures (gpu)" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
