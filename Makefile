@@ -12,7 +12,7 @@ CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip \
-            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_config.cpp \
+            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_numa.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_device.h $(wildcard $(CSRC)/coding/*.hh)
@@ -65,7 +65,7 @@ oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_ora
 tools: build/dropin_rate
 build/dropin_rate: tools/dropin_rate.cc $(LIBDIR)/libnxec.so $(HDRS)
 	@mkdir -p build
-	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread -o $@
+	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -lpthread -o $@
 
 # design probes (not product): LDS-table variants and memory-side tuning vs the product kernel
 tune: tools/microbench/tune_mul tools/microbench/lut_variants tools/microbench/shape_ceiling tools/microbench/mem_pattern tools/microbench/chunk_stride

@@ -169,10 +169,14 @@ def cpu_baseline(args, n, k, cs):
     }
     # the same legs at the cgroup's CPU count and on one thread
     quota = info.get("cgroup_cpu_quota")
+    out["at_affinity"] = {"threads": threads, "value": out["value"]}
+    out["value_leg"] = "at_affinity"
     if quota and int(quota) != threads:
         tq = max(1, int(quota))
-        r2, (e2, d2) = _cpu_legs(tq, ns, legs(level), 1.0)
+        r2, (e2, d2) = _cpu_legs(tq, ns, legs(level), args.cpu_seconds / 2)
         out["at_cgroup_quota"] = {"threads": tq, "value": round(r2 * ns * stripe_bytes / (e2 + d2) / GIB, 3)}
+        if out["at_cgroup_quota"]["value"] > out["value"]:  # report the host's better figure
+            out["value"], out["cores"], out["value_leg"] = out["at_cgroup_quota"]["value"], tq, "at_cgroup_quota"
     nss = min(ns, 16)
     r1, (e1, d1) = _cpu_legs(1, nss, legs(level), 1.0)
     out["single_thread"] = round(r1 * nss * stripe_bytes / (e1 + d1) / GIB, 3)
@@ -216,33 +220,72 @@ PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file
 }
 
 
+def lib_sha16():
+    """First 16 hex digits of the SHA-256 of the loaded libnxec.so (ties a
+    committed PMC pass to the library it measured)."""
+    import hashlib
+
+    from nexoedge_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def load_traffic(args, wl_name, launch_bytes):
     """HBM bytes per launch of the roofline kernel from the committed PMC passes
     (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 x2 read correction): the
     measured traffic/algorithmic ratio of that op's dispatches times this
-    launch's algorithmic bytes.  None when no pass covers this workload."""
+    launch's algorithmic bytes, with the PMC file and the library hash it was
+    measured on (compare with roofline.lib_sha16: a mismatch means the pass
+    predates the running library).  (None, None) when no pass covers this workload."""
     key = PMC_SUMMARIES.get((wl_name, args.chunk, args.layout))
     if key is None:
-        return None
+        return None, None
     try:
         with open(os.path.join(ROOT, "profiles", key[0])) as f:
-            ops = key[1] if isinstance(key[1], tuple) else (key[1],)
-            disp = [d for d in json.load(f)["dispatches"] if d["op"] == ops[0] or d["op"].startswith(ops[1:])]
+            doc = json.load(f)
+        ops = key[1] if isinstance(key[1], tuple) else (key[1],)
+        disp = [d for d in doc["dispatches"] if d["op"] == ops[0] or d["op"].startswith(ops[1:])]
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
     if not disp:
-        return None
+        return None, None
     ratio = sum(d["hbm_bytes"] / d["algorithmic_bytes"] for d in disp) / len(disp)
-    return int(round(ratio * launch_bytes))
+    src = {"file": "profiles/" + key[0], "lib_sha16": doc.get("lib_sha16"), "dispatches": len(disp),
+           "traffic_over_algorithmic": round(ratio, 5)}
+    return int(round(ratio * launch_bytes)), src
 
 
 class Workload:
     """One bench step = the ops in `ops`, each (label, fn(step_index), algorithmic bytes)."""
 
-    def __init__(self, name, metric, config, ops, buffers, roof_kernel, stripes, roof_ops=1):
+    def __init__(self, name, metric, config, ops, buffers, roof_kernel, stripes, roof_ops=1, erase=None):
         self.name, self.metric, self.config, self.ops = name, metric, config, ops
         self.buffers, self.roof_kernel, self.stripes = buffers, roof_kernel, stripes
         self.roof_ops = roof_ops  # the first roof_ops ops are launches of the roofline kernel
+        # erase-and-rebuild checks run after the timed region: [(label, erase(), rebuild())] on buffers[0]
+        self.erase = erase or []
+
+
+def erase_checks(wl, ctx, want):
+    """After the timed region: for each (label, erase, rebuild) the chunks are
+    really destroyed (the batch checksum must change), then rebuilt by the
+    same op the timed loop ran (it must come back to `want`, the checksum of
+    the consistent batch).  A rebuild that writes nothing fails here, which
+    re-running it on an intact batch cannot show."""
+    out = {}
+    for label, erase, rebuild in wl.erase:
+        erase()
+        ctx.sync()
+        destroyed = wl.buffers[0].checksum() != want
+        rebuild()
+        ctx.sync()
+        out[label] = bool(destroyed and wl.buffers[0].checksum() == want)
+    return out
+
+
+def _zero_chunks(buf, chunks, cst, stripe, cs, ns, stream):
+    for c in chunks:
+        buf.memset2d(0, c * cst, stripe, cs, ns, stream)
 
 
 def layout(args, n, cs):
@@ -274,11 +317,15 @@ def wl_rs10_4(args, ctx, stream, rank):
         "launch": json.loads(ctx.describe_launch(p, k, cs, ns)),
     }
     kern = config["launch"]["kernel"]
+    zero = lambda cl: _zero_chunks(buf, cl, cst, stripe, cs, ns, stream)  # noqa: E731
+    erase = [("encode", lambda: zero(range(k, n)), lambda: ops[0][1](0))]
+    for i, pat in enumerate(PATTERNS):
+        erase.append((f"recover{pat}", lambda pat=pat: zero(pat), lambda i=i: ops[1][1](i)))
     # encode and the 4-row recovers are launches of the same kernel
     # (k_mul_vec<10, 8, ...>): the roofline averages all of them, as rocprofv3's
     # per-kernel mean does
     return Workload("rs10_4", "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident", config, ops, [buf],
-                    f"{kern} K={k} rows={p} work-queue (encode + recover launches)", ns, roof_ops=2)
+                    f"{kern} K={k} rows={p} work-queue (encode + recover launches)", ns, roof_ops=2, erase=erase)
 
 
 def wl_repair12(args, ctx, stream, rank):
@@ -309,8 +356,10 @@ def wl_repair12(args, ctx, stream, rank):
               "byte_accounting": "fused (k+1)*cs; CAR unfused (k+1+2G)*cs per stripe (SURVEY 8d)",
               "launch": json.loads(ctx.describe_launch(1, k, cs, ns))}
     kern = config["launch"]["kernel"]
+    zero = lambda: _zero_chunks(buf, [failed], cst, stripe, cs, ns, stream)  # noqa: E731
+    erase = [("repair_fused", zero, lambda: ops[0][1](0)), ("repair_car_unfused", zero, lambda: unfused(0))]
     return Workload("repair12", "GiB/s RS(12,4) single-failure repair, 1 MiB chunks, device-resident", config, ops,
-                    [buf, part], f"{kern} K={k} rows=1 (fused recover)", ns)
+                    [buf, part], f"{kern} K={k} rows=1 (fused recover)", ns, erase=erase)
 
 
 def wl_mixed16(args, ctx, stream, rank):
@@ -330,8 +379,11 @@ def wl_mixed16(args, ctx, stream, rank):
                           f"(~{args.gib} GiB) per GPU",
               "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": pats, "layout": lay,
               "launch": json.loads(ctx.describe_launch(4, k, cs, ns))}
+    zero = lambda cl: _zero_chunks(buf, cl, cst, stripe, cs, ns, stream)  # noqa: E731
+    erase = [("encode", lambda: zero(range(k, n)), lambda: ops[0][1](0))]
+    erase += [(f"recover{pat}", lambda pat=pat: zero(pat), lambda i=i: ops[1][1](i)) for i, pat in enumerate(pats)]
     return Workload("mixed16", f"GiB/s RS(16,4) encode+decode, {cs >> 10} KiB chunks, device-resident", config, ops,
-                    [buf], "k_mul_vec<K=16,R=8> (encode launch)", ns)
+                    [buf], "k_mul_vec<K=16,R=8> (encode launch)", ns, erase=erase)
 
 
 def wl_write14(args, ctx, stream, rank):
@@ -609,7 +661,16 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # one rank per GPU; more ranks than visible GPUs share them round-robin
     # (only for rehearsing the multi-rank path on a small box)
-    ctx = nxec.Context(local % max(1, nxec.device_count()))
+    dev = local % max(1, nxec.device_count())
+    # before any pinned buffer or host worker thread exists: this rank's host
+    # work runs on the CPUs (and first-touch memory) of its GPU's NUMA node
+    # (the CPU baseline below runs on the process's original CPUs)
+    orig_affinity = os.sched_getaffinity(0)
+    try:
+        numa_node = nxec.bind_thread_numa(dev)
+    except nxec.NxecError:
+        numa_node = -1
+    ctx = nxec.Context(dev)
     stream = ctx.stream
     wl = WORKLOADS[args.workload](args, ctx, stream, rank)
     step_bytes = sum(b for _, _, b in wl.ops)
@@ -643,7 +704,11 @@ def main():
     grp.barrier()
     elapsed = grp.max(t1 - t0)
     total_bytes = grp.sum(float(step_bytes * args.steps))
+    numa_nodes = [int(v) for v in grp.gather(numa_node)]
     verified = grp.sum(0.0 if wl.buffers[0].checksum() == sum_before else 1.0) == 0.0
+    # outside the timed region: erase chunks for real and rebuild them
+    rebuilt = erase_checks(wl, ctx, sum_before)
+    verified = grp.sum(0.0 if verified and all(rebuilt.values()) else 1.0) == 0.0
 
     # on-box copy ceiling: hipMemcpyDtoD of 16 GiB inside the
     # workload buffer, after the checksum above (it overwrites data)
@@ -672,7 +737,7 @@ def main():
         b0 = sum(b for _, _, b in ro) // len(ro)
         ms0 = sum(op_ms[:wl.roof_ops]) / len(ro)
         gbs0 = b0 / (ms0 * 1e-3) / 1e9
-        traffic = load_traffic(args, wl.name, b0)
+        traffic, traffic_src = load_traffic(args, wl.name, b0)
         result = {
             "metric": wl.metric,
             "value": round(total_bytes / elapsed / GIB, 2),
@@ -687,7 +752,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (splitmix64 bytes, device-generated)",
             "verified": verified,
+            "verified_rebuilds": rebuilt or None,
             "config": dict(wl.config, parallelism=f"stripe-sharded x{world}, no collectives"),
+            "numa_node_per_rank": numa_nodes,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(gbs0, 1),
@@ -695,6 +762,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(gbs0 / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "lib_sha16": lib_sha16(),
                 "kernel": wl.roof_kernel,
                 "bytes_per_launch": b0,
                 "avg_launch_ms": round(ms0, 4),
@@ -716,6 +785,8 @@ def main():
             result["host_inclusive"] = hi
     if args.host_inclusive and headline_n1:
         result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
+    if (headline_n1 or (rank == 0 and world == 1 and wl.name == "config1")) and not args.no_cpu_baseline:
+        os.sched_setaffinity(0, orig_affinity)  # the host's CPUs, not only the GPU's node
     if headline_n1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args, args.n, args.k, args.chunk)
         if args.host_inclusive:

@@ -65,9 +65,12 @@ void nxec_ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbl
  *    (erasure_code.h:98) at rs.cc:89,106,230 and coding_util.hh:21,28.
  *    coding[r][i] = XOR_j c(r,j) * data[j][i], c from gftbls (byte [1]).
  *    Runs on the calling thread's current device (a per-device default
- *    context), staging through pinned memory.  The void form aborts with a
- *    message on failure (the ISA-L signature has no error channel and silent
- *    corruption is not an option); the _status form returns the error.
+ *    context), staging through pinned memory.  The ISA-L signature has no
+ *    error channel: on a device error the void form retries once on a fresh
+ *    context through the plain staged path (H2D, multiply, D2H), and aborts
+ *    with a message only when that fails too (or the arguments are invalid) --
+ *    silent corruption is not an option.  The _status form returns the error.
+ *    NXEC_TEST_FAIL_ENCODE=1 (testing) fails every first attempt.
  * ------------------------------------------------------------------------- */
 void nxec_ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
                          unsigned char **coding);
@@ -82,6 +85,17 @@ int nxec_encode_host(int len, int k, int rows, const unsigned char *coeffs, cons
  * (the unit rows of a full-output decode, rs.cc:228-230).  rows may be 0. */
 int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
                         unsigned char *const *coding, const int32_t *copy_idx, unsigned char *const *copy_out);
+/* nxec_encode_host plus the MD5 of the chunks in the same kernel pass
+ * (RSCode::encode's stripe + chunk_manager.cc:175, RSCode::decode(isRepair) +
+ * :1173, agent.cc:339 + :342): md5_data (k x 16, NULL = skip) receives the
+ * digests of the k inputs, md5_code (rows x 16, NULL = skip) those of the
+ * outputs (RFC 1321 byte order).  Pinned / registered buffers (the chunk
+ * arena) are read and written in place over PCIe by one k_gather_md5 launch;
+ * concurrent callers' calls of one chunk length are aggregated into one
+ * launch (nxec_agent_encode_batch's rounds on the thread's default context).
+ * Synchronous; thread-safe. */
+int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                         unsigned char *const *coding, unsigned char *md5_data, unsigned char *md5_code);
 
 /* ---------------------------------------------------------------------------
  * 2b. The boundary under the names of SURVEY §8b (thin forms of the above,
@@ -296,6 +310,12 @@ int nxec_encode_object(nxec_ctx_t *ctx, int n, int k, const unsigned char *d_obj
 int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream);
+/* the same with chunk (s, i) at d_chunks + s*stripe_stride + i*chunk_stride
+ * (e.g. the nxec_batch_layout(..., NXEC_LAYOUT_RECOVER_HEAVY) strides
+ * StripeBatch::decodeFile stages fetched chunks at) */
+int nxec_decode_object_ex(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                          const unsigned char *d_chunks, int64_t chunk_stride, int64_t stripe_stride, int64_t length,
+                          int64_t max_chunk_size, unsigned char *d_object, unsigned char *d_tail, void *stream);
 
 /* Read path with checksums: every chunk used as a decode input (the first k
  * alive ones of each stripe) has its MD5 checked against d_md5 ([ns][n][16],
@@ -349,8 +369,8 @@ int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *
  * getEncodedChunks, container_manager.cc:221-258: 1 x g row) or the
  * RPR_CHUNK_REQ repair (agent.cc:240-415: all-ones 1 x G for CAR, the
  * proxy's e x k matrix otherwise), plus the MD5 of every output
- * (agent.cc:342) when md5 != NULL.  Requests with the same shape and matrix
- * run as one kernel pass; staging is pinned and double-buffered so the host
+ * (agent.cc:342) when md5 != NULL (and of every input when md5_inputs !=
+ * NULL).  Requests with the same shape and matrix run as one kernel pass; staging is pinned and double-buffered so the host
  * gather of batch i+1 overlaps the GPU work of batch i.  batch_bytes bounds
  * the staging per batch (<= 0: 256 MiB).  Synchronous; thread-safe. */
 typedef struct nxec_agent_req {
@@ -360,6 +380,8 @@ typedef struct nxec_agent_req {
   const unsigned char *const *inputs; /* ninputs host chunks of chunk_size bytes */
   unsigned char *const *outputs;      /* noutputs host buffers of chunk_size bytes */
   unsigned char *md5;                 /* noutputs x 16 digest bytes, or NULL */
+  unsigned char *md5_inputs;          /* ninputs x 16 digests of the inputs, or NULL
+                                         (RSCode::encode hashes its data chunks too) */
 } nxec_agent_req;
 
 int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
@@ -453,6 +475,8 @@ int nxec_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes, void *stream);
 int nxec_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes, void *stream);
 int nxec_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes, void *stream);
 int nxec_memset(void *d_dst, int value, size_t bytes, void *stream);
+/* rows of `width` bytes, `height` of them, `pitch` apart (e.g. one chunk of every stripe) */
+int nxec_memset2d(void *d_dst, size_t pitch, int value, size_t width, size_t height, void *stream);
 int nxec_stream_create(void **stream);
 int nxec_stream_destroy(void *stream);
 int nxec_stream_sync(void *stream);
@@ -470,11 +494,25 @@ int nxec_checksum(const void *d_src, size_t bytes, uint64_t *out, void *stream);
  * replication, block/grid) -- for benchmarks and logs. */
 int nxec_describe_launch(nxec_ctx_t *ctx, int rows, int k, int64_t len, int64_t nstripes, char *buf, int buf_len);
 
+/* ---- NUMA placement (SURVEY §8e on a 2-socket host): the CPUs of the node a
+ * GPU's PCIe root sits on, read from sysfs (<NXEC_SYSFS_ROOT>/sys/bus/pci/
+ * devices/<bus id>/numa_node and /sys/devices/system/node/node<N>/cpulist).
+ * Binding restricts the CALLING THREAD (and the threads it creates later, e.g.
+ * the host worker pool) to that node's CPUs within its current affinity; the
+ * node is -1 and nothing changes when sysfs does not know it.  Group device
+ * threads bind themselves (nxec_group_*). */
+int nxec_pci_numa_node(const char *bus_id, int *node);
+int nxec_numa_node_cpus(int node, int *cpus, int max, int *count);
+int nxec_bind_thread_to_pci(const char *bus_id, int *node);
+int nxec_device_numa_node(int device, int *node);
+int nxec_bind_thread_to_device(int device, int *node);
+
 /* ---------------------------------------------------------------------------
  * 6. Pinned host arena for chunk buffers (Chunk::allocateData, reference
- *    chunk.hh:55-66).  Blocks are pinned and device-mapped, recycled by size
- *    class, never returned to the OS; the arena is bounded by
- *    NXEC_HOST_ARENA_MAX bytes (default 16 GiB, 0 disables).  nxec_encode_host
+ *    chunk.hh:55-66).  Blocks are pinned and device-mapped and recycled by
+ *    size class (nxec_host_arena_trim returns free ones to the OS); the arena
+ *    is bounded by NXEC_HOST_ARENA_MAX bytes (default: an eighth of physical
+ *    memory, at most 16 GiB; 0 disables).  nxec_encode_host
  *    (RSCode::encode, CodingUtils::encode) hands arena buffers to the GPU
  *    without a staging copy.  nxec_host_alloc fails (NXEC_ERR_NOMEM /
  *    NXEC_ERR_NODEV) when the arena is full or no device is usable: the
@@ -486,6 +524,10 @@ int nxec_host_free(void *p);
 /* 1 if p is the start of an arena block, else 0 */
 int nxec_host_arena_owns(const void *p);
 int nxec_host_arena_stats(size_t *pinned_bytes, size_t *in_use_bytes);
+/* the arena's bound in bytes */
+size_t nxec_host_arena_cap(void);
+/* unpins free blocks (largest first) until at most keep_bytes stay pinned */
+int nxec_host_arena_trim(size_t keep_bytes);
 /* 1 if the whole host range [p, p + bytes) is pinned / registered memory of
  * one device mapping -- the test the host entry points apply before letting a
  * kernel read or write a buffer over PCIe (zero copy) -- else 0 */

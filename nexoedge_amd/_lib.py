@@ -42,6 +42,7 @@ _PROTOS = {
     "nxec_ec_encode_data_status": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
     "nxec_encode_host": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
     "nxec_encode_host_ex": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
+    "nxec_encode_host_md5": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "nxec_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
     "nxec_ctx_destroy": (None, [vp]),
     "nxec_ctx_stream": (vp, [vp]),
@@ -72,6 +73,7 @@ _PROTOS = {
     "nxec_objects_layout": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_objects": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, i64, vp, vp, vp, vp]),
     "nxec_decode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp]),
+    "nxec_decode_object_ex": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, i64, vp, vp, vp]),
     "nxec_agent_encode_batch": (C.c_int, [vp, vp, C.c_int, i64, i64]),
     "nxec_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
     "nxec_gather_chunks": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
@@ -95,6 +97,7 @@ _PROTOS = {
     "nxec_memcpy_d2h": (C.c_int, [vp, vp, C.c_size_t, vp]),
     "nxec_memcpy_d2d": (C.c_int, [vp, vp, C.c_size_t, vp]),
     "nxec_memset": (C.c_int, [vp, C.c_int, C.c_size_t, vp]),
+    "nxec_memset2d": (C.c_int, [vp, C.c_size_t, C.c_int, C.c_size_t, C.c_size_t, vp]),
     "nxec_stream_create": (C.c_int, [C.POINTER(vp)]),
     "nxec_stream_destroy": (C.c_int, [vp]),
     "nxec_stream_sync": (C.c_int, [vp]),
@@ -111,6 +114,8 @@ _PROTOS = {
     "nxec_host_free": (C.c_int, [vp]),
     "nxec_host_arena_owns": (C.c_int, [vp]),
     "nxec_host_arena_stats": (C.c_int, [C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "nxec_host_arena_cap": (C.c_size_t, []),
+    "nxec_host_arena_trim": (C.c_int, [C.c_size_t]),
     "nxec_host_range_mapped": (C.c_int, [vp, C.c_size_t]),
     "nxec_chunk_md5_mode": (C.c_int, []),
     "nxec_digest_clear": (None, []),
@@ -121,6 +126,11 @@ _PROTOS = {
     "nxec_proxy_repair_using_car": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
     "nxec_reset_work_queues": (C.c_int, []),
     "nxec_debug_poison_next_queue_slot": (C.c_int, [C.c_uint32]),
+    "nxec_pci_numa_node": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
+    "nxec_numa_node_cpus": (C.c_int, [C.c_int, vp, C.c_int, C.POINTER(C.c_int)]),
+    "nxec_bind_thread_to_pci": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
+    "nxec_device_numa_node": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
+    "nxec_bind_thread_to_device": (C.c_int, [C.c_int, C.POINTER(C.c_int)]),
     "nxec_group_create": (C.c_int, [vp, C.c_int, C.POINTER(vp)]),
     "nxec_group_destroy": (None, [vp]),
     "nxec_group_size": (C.c_int, [vp]),
@@ -141,7 +151,7 @@ class StorageClass(C.Structure):
 class AgentReq(C.Structure):
     """struct nxec_agent_req of include/nxec.h"""
     _fields_ = [("ninputs", C.c_int), ("noutputs", C.c_int), ("matrix", vp), ("inputs", vp), ("outputs", vp),
-                ("md5", vp)]
+                ("md5", vp), ("md5_inputs", vp)]
 
 
 for _name, (_res, _args) in _PROTOS.items():

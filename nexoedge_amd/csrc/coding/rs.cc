@@ -55,12 +55,26 @@ bool RSCode::encode(data_t *data, length_t dataSize, std::vector<Chunk> &stripe,
   // host pool (fresh chunk buffers fault their pages in on first touch)
   nxec::host_parallel_for(k, [&](int i) { std::memcpy(stripe[i].data, data + static_cast<size_t>(i) * cs, cs); });
   if (n == k || cs == 0) return true;
-  const int rc = nxec_encode_host(static_cast<int>(cs), k, n - k, _encodeMatrix + k * k, datap.data(), codep.data());
+  // The caller hashes every chunk next (chunk_manager.cc:175): the GPU hashes
+  // all n in the encode's own pass over the arena chunks (one lane's MD5
+  // chain per chunk; the n chains run side by side), and each chunk carries
+  // its digest to Chunk::computeMD5 (chunk.hh).  NXEC_CHUNK_MD5=0: no digests.
+  const bool digests = nxec_chunk_md5_mode() >= 1;
+  std::vector<unsigned char> md5(digests ? static_cast<size_t>(n) * 16 : 0);
+  const int rc = digests ? nxec_encode_host_md5(static_cast<int>(cs), k, n - k, _encodeMatrix + k * k, datap.data(),
+                                                codep.data(), md5.data(), md5.data() + 16 * k)
+                         : nxec_encode_host(static_cast<int>(cs), k, n - k, _encodeMatrix + k * k, datap.data(),
+                                            codep.data());
   if (rc != NXEC_OK) {
     std::fprintf(stderr, "RSCode::encode: %s\n", nxec_last_error());
     stripe.clear();
     return false;
   }
+  if (digests)
+    for (int i = 0; i < n; i++) {
+      std::memcpy(stripe[i].md5, md5.data() + 16 * i, 16);
+      stripe[i].setDigestValid();
+    }
   return true;
 }
 
@@ -133,9 +147,17 @@ bool RSCode::decode(std::vector<Chunk> &inputChunks, data_t **decodedData, lengt
     std::vector<unsigned char> m(static_cast<size_t>(tg.size()) * k + 1);
     if (nxec_rs_decode_matrix(n, k, ids.data(), tg.data(), static_cast<int>(tg.size()), m.data()) != NXEC_OK)
       return fail();
-    if (nxec_encode_host(static_cast<int>(cs), k, static_cast<int>(tg.size()), m.data(), inputp.data(),
-                         decodep.data()) != NXEC_OK)
+    // NXEC_CHUNK_MD5=2: the repaired chunks' digests from the same pass, for
+    // the computeMD5 of each at chunk_manager.cc:1170-1173 (regions of *decodedData)
+    const bool digests = nxec_chunk_md5_mode() >= 2 && !tg.empty();
+    std::vector<unsigned char> md5(digests ? tg.size() * 16 : 0);
+    if (digests) nxec_digest_clear();
+    if ((digests ? nxec_encode_host_md5(static_cast<int>(cs), k, static_cast<int>(tg.size()), m.data(), inputp.data(),
+                                        decodep.data(), nullptr, md5.data())
+                 : nxec_encode_host(static_cast<int>(cs), k, static_cast<int>(tg.size()), m.data(), inputp.data(),
+                                    decodep.data())) != NXEC_OK)
       return fail();
+    for (size_t t = 0; digests && t < tg.size(); t++) nxec_digest_note(decodep[t], cs, md5.data() + 16 * t);
   } else {
     // all k data chunks (rs.cc:228-230 with the k x k inverse): the rows of
     // the inverse for erased data ids run on the GPU; the unit rows of the

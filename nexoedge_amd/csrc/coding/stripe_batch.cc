@@ -91,7 +91,10 @@ bool StripeBatch::encodeFile(const data_t *data, uint64_t length, length_t maxCh
       c.data = d;
       c.size = static_cast<int>(cs);
       c.freeData = false;  // views into the file buffer / this batch
-      if (computeMD5) std::memcpy(c.md5, _md5 + (s * n + i) * 16, 16);
+      if (computeMD5) {  // chunk_manager.cc:175's computeMD5 then returns the GPU digest
+        std::memcpy(c.md5, _md5 + (s * n + i) * 16, 16);
+        c.setDigestValid();
+      }
     }
   }
   return true;
@@ -117,26 +120,32 @@ bool StripeBatch::decodeFile(std::vector<Chunk> &inputs, uint64_t length, length
       const int64_t want = s < nf ? M : cl;
       if (c.chunkId % n != ids[j] || c.size != want || !c.data) return false;  // decodeFile's id use, :775
     }
-  if (!growDevice(&_dChunks, &_dChunksCap, static_cast<size_t>(ns) * n * M) ||
+  // the staged stripes sit at the library's recover-heavy strides
+  // (nxec_batch_layout): a degraded read's survivors are read with holes
+  // ({1,4,11,13} lost), which the packed [s][n][M] layout serves at ~0.71 of
+  // 8 TB/s and the padded stripe stride at ~0.78
+  int64_t cst = M, sst = int64_t(n) * M;
+  if (nxec_batch_layout(n, M, NXEC_LAYOUT_RECOVER_HEAVY, &cst, &sst) != NXEC_OK) return false;
+  if (!growDevice(&_dChunks, &_dChunksCap, static_cast<size_t>(ns) * sst) ||
       !growDevice(&_dObject, &_dObjectCap, static_cast<size_t>(length)) ||
       !growDevice(&_dTail, &_dTailCap, static_cast<size_t>(k) * M))
     return false;
   void *st = nxec_ctx_stream(_ctx);
-  // fetched chunks -> [s][n][M] in HBM, one gather per (chunk id, stripe kind)
+  // fetched chunks -> HBM, one gather per (chunk id, stripe kind)
   std::vector<const unsigned char *> frames;
   for (int j = 0; j < k; j++) {
     frames.clear();
     for (int64_t s = 0; s < nf; s++) frames.push_back(inputs[static_cast<size_t>(s) * k + j].data);
-    if (nf > 0 && nxec_gather_chunks(_ctx, frames.data(), nf, M, _dChunks + ids[j] * M, n * M, st) != NXEC_OK)
+    if (nf > 0 && nxec_gather_chunks(_ctx, frames.data(), nf, M, _dChunks + ids[j] * cst, sst, st) != NXEC_OK)
       return false;
     if (ns > nf) {
       const unsigned char *fr = inputs[static_cast<size_t>(nf) * k + j].data;
-      if (nxec_gather_chunks(_ctx, &fr, 1, cl, _dChunks + (nf * n + ids[j]) * M, M, st) != NXEC_OK) return false;
+      if (nxec_gather_chunks(_ctx, &fr, 1, cl, _dChunks + nf * sst + ids[j] * cst, M, st) != NXEC_OK) return false;
     }
   }
   // decodeFile for every stripe (chunk_manager.cc:738-800), straight into the object
-  if (nxec_decode_object(_ctx, n, k, f.data(), static_cast<int>(f.size()), _dChunks, static_cast<int64_t>(length), M,
-                         _dObject, _dTail, st) != NXEC_OK)
+  if (nxec_decode_object_ex(_ctx, n, k, f.data(), static_cast<int>(f.size()), _dChunks, cst, sst,
+                            static_cast<int64_t>(length), M, _dObject, _dTail, st) != NXEC_OK)
     return false;
   if (nxec_memcpy_d2h(out, _dObject, static_cast<size_t>(length), st) != NXEC_OK) return false;
   return nxec_stream_sync(st) == NXEC_OK;

@@ -39,7 +39,9 @@
 #include <algorithm>
 #include <array>
 #include <cstdlib>
+#include <queue>
 #include <utility>
+#include <vector>
 
 #include "nxec_device.h"
 #include "nxec_internal.h"
@@ -402,10 +404,14 @@ constexpr int gm_depth() {
 // usually holds fewer requests than it has code lanes: the idle lanes read
 // and write `scratch` in HBM (one address per lane) instead of shadowing a
 // live request, which would multiply its PCIe reads.
-template <int K>
+// HSRC: the sources are hashed too (RSCode::encode's n digests per stripe,
+// chunk_manager.cc:175): rows 0..K-1 of a request are its sources, then its
+// outputs -- a template parameter for the reason k_mul_md5's is.
+template <int K, bool HSRC>
 __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int nh = a.p;
+  constexpr int hsrc = HSRC ? K : 0;  // rows before the outputs' rows
+  const int nh = hsrc + a.p;
   const int S = a.stripes_per_group;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
@@ -448,6 +454,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
       for (int i = 0; i < 16; i++) acc[i] = 0;
 #pragma unroll
       for (int j = 0; j < K; j += 2) {
+        if (HSRC && act) {
+          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
+        }
         lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
@@ -459,7 +469,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
           dev::st_stream(dp[r] + step * sstep, pv);
-          if (act) *reinterpret_cast<u32x4 *>(rb + r * kEmRow) = pv;
+          if (act) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;
         }
       }
       lds_barrier();
@@ -507,6 +517,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
         }
       }
       uint8_t *rb = row + (nfull & 1) * buf_bytes;
+      if (HSRC && act) {  // zero past the end, as the hash lanes' padding expects
+#pragma unroll
+        for (int j = 0; j < K; j++) *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
+      }
       uint32_t acc[16];
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = 0;
@@ -524,7 +538,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
             const uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
             for (int i = 0; i < nb; i++) dp[r][off + i] = static_cast<uint8_t>(w[i / 4] >> (8 * (i % 4)));
           }
-          if (act) *reinterpret_cast<u32x4 *>(rb + r * kEmRow) = pv;  // zero past the end: GF products of zeros
+          if (act) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;  // zero past the end: GF products of zeros
         }
       }
       lds_barrier();
@@ -544,129 +558,94 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
   }
 }
 
-// Hash waves of k_files_md5: hash_rows with a length per lane.  Lane h's
-// chunk has my_steps steps, the last holding my_tail bytes (1..256; the row's
-// bytes past them are masked off here, so the code lanes need not zero them);
-// the workgroup runs nsteps >= my_steps steps (its longest request), and a
-// lane that is done only keeps the barriers.  st comes back finished (RFC
-// 1321 padding built in registers).
-__device__ __forceinline__ void hash_rows_var(const uint8_t *buf, uint32_t buf_bytes, int h, bool active, int nsteps,
-                                              int my_steps, int my_tail, uint64_t len, uint32_t (&st)[4]) {
-  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
-  md5_init(st);
-  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
-    const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
-#pragma unroll
-    for (int i = 0; i < kEmVecs; i++) {
-      const u32x4 x = p[i];
-      m[4 * i] = x.x;
-      m[4 * i + 1] = x.y;
-      m[4 * i + 2] = x.z;
-      m[4 * i + 3] = x.w;
-    }
-  };
-  auto proc = [&](int t, const uint32_t(&m)[kEncMd5Step / 4]) {
-    if (!active || t >= my_steps) return;
-    if (t < my_steps - 1) {
-#pragma unroll
-      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
-      return;
-    }
-    const int fb = my_tail / 64, r = my_tail % 64;
-#pragma unroll
-    for (int b = 0; b < kEncMd5Step / 64; b++)
-      if (b < fb) md5_block(st, m + 16 * b);
-    uint32_t w[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int b = 0; b < kEncMd5Step / 64; b++)
-        if (b == fb) x = m[16 * b + i];
-      // keep the word's bytes below r, then the 0x80 terminator
-      const int keep = r - 4 * i;  // bytes of this word inside the chunk
-      const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
-      w[i] = (x & mask) | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
-    }
-    const uint32_t lo = static_cast<uint32_t>(len * 8), hi = static_cast<uint32_t>((len * 8) >> 32);
-    if (r >= 56) {
-      md5_block(st, w);
-#pragma unroll
-      for (int i = 0; i < 16; i++) w[i] = 0;
-    }
-    w[14] = lo;
-    w[15] = hi;
-    md5_block(st, w);
-  };
-  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
-  lds_barrier();
-  if (active) fetch(0, m0);
-  int step = 1;
-  for (; step + 2 <= nsteps; step += 2) {
-    lds_barrier();
-    if (active && step < my_steps) fetch(step, m1);
-    proc(step - 1, m0);
-    lds_barrier();
-    if (active && step + 1 < my_steps) fetch(step + 1, m0);
-    proc(step, m1);
-  }
-  if (step < nsteps) {
-    lds_barrier();
-    if (active && step < my_steps) fetch(step, m1);
-    proc(step - 1, m0);
-    proc(step, m1);
-  } else {
-    proc(step - 1, m0);
-  }
-}
-
 // The multi-file write in one launch (nxec_encode_objects; the per-file
 // loop of Proxy::writeFileStripes, proxy_file_ops.cc:557-666, with
 // writeFileStripe's encode + Chunk::computeMD5 of all n chunks,
 // chunk_manager.cc:66-452): k_mul_md5's code/hash split over pointer tables,
 // every request (a full stripe read in place from its object, or a file's
 // zero-padded last stripe in the tail arena) with its own chunk length.
-// Requests come sorted longest first, so a workgroup's first request sets its
-// step count; a lane past its request's end re-reads its last in-bounds
-// vector, stores to scratch and leaves its LDS row alone (the hash lanes mask
-// the bytes past a chunk's end).
+//
+// Requests are packed into slots (plan_files_slots): a slot is one stripe's
+// worth of lanes -- 16 code lanes, k + p hash lanes -- that runs its requests
+// back to back.  A batch of 6 000 requests on 256 CUs x 16 slots used to need
+// a second wave of workgroups (18.8 ms for 4096 files of 1 B - 20 MiB); with
+// the requests spread so that every slot's chains add up to about the
+// longest one, it runs in one wave.  Per lane, a cursor (request of the
+// slot's list, step inside it) replaces the fixed request: the load cursor
+// runs D - 1 steps ahead of the compute cursor through the register ring,
+// and at a request boundary a lane takes the next request's pointers from
+// the workgroup's request table in LDS (no global load in the loop, so the
+// ring's vmcnt bookkeeping is unchanged).  A hash lane finishes its chunk's
+// digest at the request's last step (RFC 1321 padding built in registers,
+// bytes past the chunk's end masked off) and starts the next chain at once.
+// A lane past its request's end in that request's last step re-reads its
+// last in-bounds vector, stores to scratch and leaves its LDS row alone.
 template <int K>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = K + a.p;
-  const int S = a.stripes_per_group;
+  const int S = a.slots_per_group;
+  const int L = a.max_list;
+  const int rec = K + a.p + 2;  // request record: K sources, p outputs, digest base, length
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
   const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
+  uint64_t *rq = reinterpret_cast<uint64_t *>(buf + 2 * buf_bytes);  // [S][L][rec]
   build_tables<1>(a.coef, K, a.p, tab);
+  const int64_t g0 = static_cast<int64_t>(blockIdx.x) * S;
+  const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nslots - g0));
+  for (int i = threadIdx.x; i < nS * L * rec; i += kEmBlock) {
+    const int ls = i / (L * rec), li = (i / rec) % L, f = i % rec;
+    const int first = a.slot_first[g0 + ls], cnt = a.slot_first[g0 + ls + 1] - first;
+    uint64_t v = 0;
+    if (li < cnt) {
+      const int64_t r = a.slot_reqs[first + li];
+      if (f < K)
+        v = reinterpret_cast<uint64_t>(a.src_ptrs[r * K + f]);
+      else if (f < K + a.p)
+        v = reinterpret_cast<uint64_t>(a.dst_ptrs[r * a.p + (f - K)]);
+      else if (f == K + a.p)
+        v = reinterpret_cast<uint64_t>(a.dig_ptrs[r]);
+      else
+        v = static_cast<uint64_t>(a.lens[r]);
+    }
+    rq[i] = v;
+  }
   __syncthreads();
-  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
-  const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
-  const int nsteps = static_cast<int>((a.lens[s0] + kEncMd5Step - 1) / kEncMd5Step);
+  const int nsteps = a.wg_steps[blockIdx.x];
+  auto steps_of = [](int64_t len) { return static_cast<int>((len + kEncMd5Step - 1) / kEncMd5Step); };
 
   if (threadIdx.x < kEmCodeLanes) {
-    if ((threadIdx.x & ~63) >= nS * kEmVecs) {  // no live request in this wave: barriers only
+    if ((threadIdx.x & ~63) >= nS * kEmVecs) {  // no live slot in this wave: barriers only
       for (int s = 0; s < nsteps; s++) lds_barrier();
       return;
     }
     const int item = threadIdx.x;
     const bool act = item < nS * kEmVecs;
     const int ls = act ? item / kEmVecs : 0, v = item % kEmVecs;
-    const int64_t sx = s0 + ls;
-    const int64_t vlen = act ? (a.lens[sx] + 15) / 16 * 16 : 0;
-    // last step with bytes of this lane's column (-1: none)
-    const int tmax = vlen > v * 16 ? static_cast<int>((vlen - 1 - v * 16) / kEncMd5Step) : -1;
-    const int tcl = tmax < 0 ? 0 : tmax;
+    const int cnt = act ? a.slot_first[g0 + ls + 1] - a.slot_first[g0 + ls] : 1;
+    const uint64_t *q = rq + static_cast<int64_t>(ls) * L * rec;
+    auto len_of = [&](int li) { return act ? static_cast<int64_t>(q[li * rec + K + a.p + 1]) : int64_t(16); };
+    // last step with bytes of this lane's 16-byte column (-1: none)
+    auto tmax_of = [&](int64_t len) {
+      const int64_t vlen = (len + 15) / 16 * 16;
+      return vlen > v * 16 ? static_cast<int>((vlen - 1 - v * 16) / kEncMd5Step) : -1;
+    };
+    // load cursor: request lr of the slot, step lt of it
+    int lr = 0, lt = 0;
+    int64_t len0 = len_of(0);
+    int lT = steps_of(len0), ltcl = max(tmax_of(len0), 0);
     const uint8_t *sp[K];
+    // a lane whose column holds no byte of the request (chunks under 256
+    // bytes) reads the scratch line: nothing past a chunk's 16-byte padding is read
+    auto set_src = [&](int li, bool has) {
 #pragma unroll
-    for (int j = 0; j < K; j++) sp[j] = tmax >= 0 ? a.src_ptrs[sx * K + j] + v * 16 : a.scratch + v * 16;
-    uint8_t *dp[kMaxRowsPerPass];
-#pragma unroll
-    for (int r = 0; r < kMaxRowsPerPass; r++)
-      dp[r] = tmax >= 0 && r < a.p ? a.dst_ptrs[sx * a.p + r] + v * 16 : a.scratch + 256 * (r + 1) + v * 16;
-    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
-    auto load = [&](int step, u32x4(&d)[K]) {
-      const int64_t off = static_cast<int64_t>(min(step, tcl)) * kEncMd5Step;
+      for (int j = 0; j < K; j++)
+        sp[j] = act && has ? reinterpret_cast<const uint8_t *>(q[li * rec + j]) + v * 16 : a.scratch + v * 16;
+    };
+    set_src(0, tmax_of(len0) >= 0);
+    auto load = [&](u32x4(&d)[K]) {
+      const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
 #pragma unroll
       for (int j = 0; j < K; j++) {
         // plain (cached) loads: a chunk that is not 128-byte aligned (a tail
@@ -678,9 +657,32 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         else
           d[j] = dev::ld_stream(sp[j] + off);
       }
+      if (++lt == lT) {
+        if (lr + 1 < cnt) {  // next request of the slot (pointers from the LDS table)
+          lr++;
+          lt = 0;
+          const int64_t ln = len_of(lr);
+          lT = steps_of(ln);
+          ltcl = max(tmax_of(ln), 0);
+          set_src(lr, tmax_of(ln) >= 0);
+        } else {
+          lt = lT - 1;  // past the slot's end: re-read the last step
+        }
+      }
     };
+    // compute cursor
+    int cr = 0, ct = 0, cT = lT, ctmax = act ? tmax_of(len0) : -1;
+    bool live = act;
+    uint8_t *dp[kMaxRowsPerPass];
+    auto set_dst = [&](int li) {
+#pragma unroll
+      for (int r = 0; r < kMaxRowsPerPass; r++)
+        dp[r] = act && r < a.p ? reinterpret_cast<uint8_t *>(q[li * rec + K + r]) + v * 16 : a.scratch;
+    };
+    set_dst(0);
+    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
     auto run = [&](int step, const u32x4(&d)[K]) {
-      const bool ok = step <= tmax;
+      const bool ok = live && ct <= ctmax;
       uint8_t *rb = row + (step & 1) * buf_bytes;
       uint32_t acc[16];
 #pragma unroll
@@ -697,7 +699,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       }
       uint32_t o[4][4];
       rows_of(acc, o);
-      const int64_t off = static_cast<int64_t>(step) * kEncMd5Step;
+      const int64_t off = static_cast<int64_t>(ct) * kEncMd5Step;
 #pragma unroll
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
@@ -707,17 +709,28 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         }
       }
       lds_barrier();
+      if (live && ++ct == cT) {
+        if (cr + 1 < cnt) {
+          cr++;
+          ct = 0;
+          const int64_t ln = len_of(cr);
+          cT = steps_of(ln);
+          ctmax = tmax_of(ln);
+          set_dst(cr);
+        } else {
+          live = false;
+        }
+      }
     };
     constexpr int D = gm_depth<K>();
     u32x4 ring[D][K];
-    const int last = nsteps - 1;
 #pragma unroll
-    for (int j = 0; j < D - 1; j++) load(min(j, last), ring[j]);
+    for (int j = 0; j < D - 1; j++) load(ring[j]);
     int step = 0;
     for (; step + D <= nsteps; step += D) {
 #pragma unroll
       for (int j = 0; j < D; j++) {
-        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        load(ring[(j + D - 1) % D]);
         __builtin_amdgcn_sched_barrier(0);
         run(step + j, ring[j]);
       }
@@ -725,7 +738,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
 #pragma unroll
     for (int j = 0; j < D - 1; j++) {
       if (step + j < nsteps) {
-        load(min(step + j + D - 1, last), ring[(j + D - 1) % D]);
+        load(ring[(j + D - 1) % D]);
         __builtin_amdgcn_sched_barrier(0);
         run(step + j, ring[j]);
       }
@@ -733,17 +746,97 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     return;
   }
 
+  // ---- hash lanes: lane h = chunk c of slot ls = LDS row h; one chain per request of the slot ----
   const int h = threadIdx.x - kEmCodeLanes;
   const bool active = h < nS * nh;
-  const int64_t my_len = active ? a.lens[s0 + h / nh] : 1;
-  const int my_steps = static_cast<int>((my_len + kEncMd5Step - 1) / kEncMd5Step);
-  const int my_tail = static_cast<int>(my_len - static_cast<int64_t>(my_steps - 1) * kEncMd5Step);
+  const int ls = active ? h / nh : 0, c = active ? h - (h / nh) * nh : 0;
+  const int cnt = active ? a.slot_first[g0 + ls + 1] - a.slot_first[g0 + ls] : 0;
+  const uint64_t *q = rq + static_cast<int64_t>(ls) * L * rec;
+  int hr = 0, ht = 0;
+  int64_t hlen = active ? static_cast<int64_t>(q[K + a.p + 1]) : 1;
+  int hT = steps_of(hlen);
+  bool live = active;
   uint32_t st[4];
-  hash_rows_var(buf, buf_bytes, h, active, nsteps, my_steps, my_tail, static_cast<uint64_t>(my_len), st);
-  if (active) {
-    uint8_t *out = a.dig_ptrs[s0 + h / nh] + (h % nh) * 16;
+  md5_init(st);
+  const u32x4 *rowp = reinterpret_cast<const u32x4 *>(buf + h * kEmRow);
+  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
+    const u32x4 *p = rowp + (step & 1) * (buf_bytes / 16);
+#pragma unroll
+    for (int i = 0; i < kEmVecs; i++) {
+      const u32x4 x = p[i];
+      m[4 * i] = x.x;
+      m[4 * i + 1] = x.y;
+      m[4 * i + 2] = x.z;
+      m[4 * i + 3] = x.w;
+    }
+  };
+  auto proc = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
+    if (!live) return;
+    if (ht < hT - 1) {
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+      ht++;
+      return;
+    }
+    // the request's last step: its tail bytes, then RFC 1321 §3.1-3.2 padding
+    const int my_tail = static_cast<int>(hlen - static_cast<int64_t>(hT - 1) * kEncMd5Step);
+    const int fb = my_tail / 64, r = my_tail % 64;
+#pragma unroll
+    for (int b = 0; b < kEncMd5Step / 64; b++)
+      if (b < fb) md5_block(st, m + 16 * b);
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int b = 0; b < kEncMd5Step / 64; b++)
+        if (b == fb) x = m[16 * b + i];
+      // keep the word's bytes below r, then the 0x80 terminator
+      const int keep = r - 4 * i;  // bytes of this word inside the chunk
+      const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+      w[i] = (x & mask) | (i == r / 4 ? 0x80u << (8 * (r % 4)) : 0u);
+    }
+    const uint64_t bits = static_cast<uint64_t>(hlen) * 8;
+    if (r >= 56) {
+      md5_block(st, w);
+#pragma unroll
+      for (int i = 0; i < 16; i++) w[i] = 0;
+    }
+    w[14] = static_cast<uint32_t>(bits);
+    w[15] = static_cast<uint32_t>(bits >> 32);
+    md5_block(st, w);
+    uint8_t *out = reinterpret_cast<uint8_t *>(q[hr * rec + K + a.p]) + c * 16;
 #pragma unroll
     for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+    md5_init(st);
+    if (hr + 1 < cnt) {
+      hr++;
+      ht = 0;
+      hlen = static_cast<int64_t>(q[hr * rec + K + a.p + 1]);
+      hT = steps_of(hlen);
+    } else {
+      live = false;
+    }
+  };
+  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
+  lds_barrier();
+  if (active) fetch(0, m0);
+  int step = 1;
+  for (; step + 2 <= nsteps; step += 2) {
+    lds_barrier();
+    if (active) fetch(step, m1);
+    proc(m0);
+    lds_barrier();
+    if (active) fetch(step + 1, m0);
+    proc(m1);
+  }
+  if (step < nsteps) {
+    lds_barrier();
+    if (active) fetch(step, m1);
+    proc(m0);
+    proc(m1);
+  } else {
+    proc(m0);
   }
 }
 
@@ -755,11 +848,13 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int
 const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
 
 using GmKernel = void (*)(const GatherMd5Args);
-template <int... Ks>
+template <bool HSRC, int... Ks>
 constexpr std::array<GmKernel, sizeof...(Ks)> gm_table(std::integer_sequence<int, Ks...>) {
-  return {{&k_gather_md5<Ks + 1>...}};
+  return {{&k_gather_md5<Ks + 1, HSRC>...}};
 }
-const std::array<GmKernel, kGatherMd5MaxK> kGm = gm_table(std::make_integer_sequence<int, kGatherMd5MaxK>{});
+// [hash_src][k - 1]
+const std::array<GmKernel, kGatherMd5MaxK> kGm[2] = {gm_table<false>(std::make_integer_sequence<int, kGatherMd5MaxK>{}),
+                                                     gm_table<true>(std::make_integer_sequence<int, kGatherMd5MaxK>{})};
 
 using EmKernel = void (*)(const MulMd5Args);
 template <bool HSRC, int... Ks>
@@ -809,7 +904,14 @@ int prepare_encode_md5() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5): %s", hipGetErrorString(e));
   }
-  for (GmKernel fn : kGm) {
+  for (GmKernel fn : kGm[0]) {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
+      return set_error(NXEC_ERR_HIP, "k_gather_md5: static LDS present (the tables must start at LDS byte 0)");
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_gather_md5): %s", hipGetErrorString(e));
+  }
+  for (GmKernel fn : kGm[1]) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
       return set_error(NXEC_ERR_HIP, "k_gather_md5: static LDS present (the tables must start at LDS byte 0)");
@@ -852,23 +954,100 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_mul_md5: %s", hipGetErrorString(e));
 }
 
+void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cus, std::vector<int32_t> &slot_first,
+                      std::vector<int32_t> &slot_reqs, std::vector<int32_t> &wg_steps, FilesMd5Args &a) {
+  const int nh = k + p;
+  const int64_t R = static_cast<int64_t>(lens.size());
+  const int64_t Smax = std::min(kEmMaxStripes, kEmMaxRows / nh);
+  const int64_t cus = std::max(num_cus, 1);
+  const char *pe = std::getenv("NXEC_FILES_PACK");
+  const bool pack = !(pe && pe[0] == '0');
+  auto steps = [](int64_t len) { return (len + kEncMd5Step - 1) / kEncMd5Step; };
+  // at most one workgroup per CU (its LDS), so 256 x Smax slots in one wave:
+  // fewer requests than that get a slot each, spread over every CU first
+  int64_t G, S;
+  if (!pack || R <= cus * Smax) {
+    G = R;
+    S = std::min<int64_t>(Smax, (R + cus - 1) / cus);
+  } else {
+    G = cus * Smax;
+    S = Smax;
+  }
+  S = std::max<int64_t>(S, 1);
+  const int64_t lds_free = kEmLds - int64_t(k) * 1024 - 2 * S * nh * kEmRow;
+  const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 2) * 8));
+  std::vector<std::vector<int32_t>> lists(static_cast<size_t>(G));
+  std::vector<int64_t> load(static_cast<size_t>(G), 0);
+  if (G == R) {
+    for (int64_t r = 0; r < R; r++) {
+      lists[static_cast<size_t>(r)].push_back(static_cast<int32_t>(r));
+      load[static_cast<size_t>(r)] = steps(lens[static_cast<size_t>(r)]);
+    }
+  } else {
+    // longest request first into the least loaded slot (LPT); a slot whose
+    // list fills the LDS request table takes no more; when every slot is
+    // full a new one opens (a second wave of workgroups)
+    typedef std::pair<int64_t, int64_t> Item;  // (load, slot)
+    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
+    for (int64_t g = 0; g < G; g++) heap.push(Item(0, g));
+    for (int64_t r = 0; r < R; r++) {
+      int64_t g = -1;
+      while (!heap.empty()) {
+        const Item it = heap.top();
+        heap.pop();
+        if (static_cast<int64_t>(lists[static_cast<size_t>(it.second)].size()) < Lmax) {
+          g = it.second;
+          break;
+        }
+      }
+      if (g < 0) {
+        g = G++;
+        lists.emplace_back();
+        load.push_back(0);
+      }
+      lists[static_cast<size_t>(g)].push_back(static_cast<int32_t>(r));
+      load[static_cast<size_t>(g)] += steps(lens[static_cast<size_t>(r)]);
+      heap.push(Item(load[static_cast<size_t>(g)], g));
+    }
+  }
+  slot_first.assign(1, 0);
+  slot_reqs.clear();
+  int64_t maxl = 1;
+  for (const auto &l : lists) {
+    slot_reqs.insert(slot_reqs.end(), l.begin(), l.end());
+    slot_first.push_back(static_cast<int32_t>(slot_reqs.size()));
+    maxl = std::max<int64_t>(maxl, static_cast<int64_t>(l.size()));
+  }
+  const int64_t nwg = (G + S - 1) / S;
+  wg_steps.assign(static_cast<size_t>(nwg), 0);
+  for (int64_t g = 0; g < G; g++) {
+    int32_t &w = wg_steps[static_cast<size_t>(g / S)];
+    w = std::max<int32_t>(w, static_cast<int32_t>(load[static_cast<size_t>(g)]));
+  }
+  a.nslots = G;
+  a.slots_per_group = static_cast<int32_t>(S);
+  a.max_list = static_cast<int32_t>(maxl);
+}
+
 int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
-  if (in.nstripes <= 0) return NXEC_OK;
+  if (in.nslots <= 0) return NXEC_OK;
   if (in.k < 1 || in.k > kFilesMd5MaxK || in.p < 1 || in.p > kMaxRowsPerPass || !in.src_ptrs || !in.dst_ptrs ||
-      !in.lens || !in.dig_ptrs || !in.scratch)
+      !in.lens || !in.dig_ptrs || !in.scratch || !in.slot_first || !in.slot_reqs || !in.wg_steps ||
+      in.slots_per_group < 1 || in.max_list < 1)
     return set_error(NXEC_ERR_INVALID, "files+md5: unsupported arguments");
   FilesMd5Args a = in;
   a.cached_loads = 1;  // FETCH x2 60.0 -> 43.6 GB per 4096-file batch (= the data bytes), same time
   if (const char *e = std::getenv("NXEC_FILES_LOADS")) a.cached_loads = e[0] != '0';
+  (void)num_cus;
   const int nh = a.k + a.p;
-  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / nh);
-  const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
-  if (per_cu < S) S = per_cu;
-  a.stripes_per_group = static_cast<int32_t>(S);
-  const int64_t grid = (a.nstripes + S - 1) / S;
+  const int64_t S = a.slots_per_group;
+  if (S * nh > kEmMaxRows || S * kEmVecs > kEmCodeLanes)
+    return set_error(NXEC_ERR_INVALID, "files+md5: %lld slots of %d chunks per workgroup", static_cast<long long>(S), nh);
+  const int64_t grid = (a.nslots + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
-  const int lds = a.k * 1024 + static_cast<int>(2 * S * nh * kEmRow);
-  hipLaunchKernelGGL(kFm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
+  const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 2) * 8;
+  if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
+  hipLaunchKernelGGL(kFm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_files_md5: %s", hipGetErrorString(e));
@@ -880,16 +1059,17 @@ int launch_gather_md5(const GatherMd5Args &in, int num_cus, void *stream) {
       in.len / kEncMd5Step >= (int64_t(1) << 31) - 1 || !in.src_ptrs || !in.dst_ptrs || !in.digests || !in.scratch)
     return set_error(NXEC_ERR_INVALID, "gather+md5: unsupported arguments");
   GatherMd5Args a = in;
+  const int nh = (a.hash_src ? a.k : 0) + a.p;  // hashed chunks per request
   // spread the requests over every CU first (each is one ~9 ms chain per
   // 1 MiB whatever the batch), then pack up to 16 per workgroup
-  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / a.p);
+  int64_t S = std::min(kEmMaxStripes, kEmMaxRows / nh);
   const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
   if (per_cu < S) S = per_cu;
   a.stripes_per_group = static_cast<int32_t>(S);
   const int64_t grid = (a.nstripes + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "gather+md5: batch too large for one launch");
-  const int lds = a.k * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
-  hipLaunchKernelGGL(kGm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
+  const int lds = a.k * 1024 + static_cast<int>(2 * S * nh * kEmRow);
+  hipLaunchKernelGGL(kGm[a.hash_src ? 1 : 0][a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_gather_md5: %s", hipGetErrorString(e));

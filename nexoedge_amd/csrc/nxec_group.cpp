@@ -2,16 +2,25 @@
 // stripes of a batch split into contiguous ranges (sizes differ by at most
 // one, as nexoedge_amd/dist.py shard_range), one host thread per device
 // driving its own streams.  Stripes are independent, so there is no
-// collective and no peer traffic: each device codes its own range.
+// collective and no peer traffic: each device codes its own range.  Each
+// device thread runs on the CPUs of its GPU's NUMA node (nxec_numa.cpp), so
+// its staging copies and zero-copy PCIe traffic stay on that socket.
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "nxec_internal.h"
 
+namespace nxec {
+std::vector<int> pci_node_cpus(const char *bus_id, int *node);
+bool bind_thread_cpus(const std::vector<int> &cpus);
+int device_bus_id(int device, char *buf, int len);
+}  // namespace nxec
+
 struct nxec_group {
   std::vector<nxec_ctx_t *> ctxs;
   std::vector<int> devices;
+  std::vector<std::vector<int>> cpus;  // per device: its NUMA node's CPUs (empty: unknown)
 };
 
 namespace {
@@ -33,6 +42,7 @@ int run_all(nxec_group *g, F fn) {
   std::vector<std::thread> th;
   for (int i = 0; i < nd; i++)
     th.emplace_back([&, i] {
+      (void)nxec::bind_thread_cpus(g->cpus[i]);
       rc[i] = fn(i);
       if (rc[i] != NXEC_OK) msg[i] = nxec_last_error();
     });
@@ -59,6 +69,10 @@ int nxec_group_create(const int *devices, int ndevices, nxec_group_t **out) {
     }
     g->ctxs.push_back(c);
     g->devices.push_back(devices[i]);
+    char bus[64] = {0};
+    int node = -1;
+    g->cpus.push_back(nxec::device_bus_id(devices[i], bus, sizeof(bus)) == NXEC_OK ? nxec::pci_node_cpus(bus, &node)
+                                                                                   : std::vector<int>());
   }
   *out = g;
   return NXEC_OK;

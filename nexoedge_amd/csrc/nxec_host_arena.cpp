@@ -10,13 +10,19 @@
 // PCIe (zero copy) or the copy engines DMA them with no host memcpy.
 //
 // Design: size classes (2^i and 1.5*2^i bytes, 4 KiB .. 1 GiB), one free list
-// per class, blocks pinned once with hipHostMalloc and recycled forever (a
-// chunk's lifetime is one request; pinning costs far more than reuse).  The
-// arena is bounded (NXEC_HOST_ARENA_MAX bytes, default 16 GiB): past the
-// bound, or without a usable device, nxec_host_alloc fails and the caller
-// falls back to ordinary memory.  Ownership lookup is a map of block start ->
-// class under one mutex (a few hundred ns, once per allocate/free).
+// per class, blocks pinned once with hipHostMalloc and recycled (a chunk's
+// lifetime is one request; pinning costs far more than reuse).  The arena is
+// bounded: NXEC_HOST_ARENA_MAX bytes, by default an eighth of the host's
+// physical memory and at most 16 GiB (pinned pages cannot be swapped or
+// reclaimed).  Past the bound, or without a usable device, nxec_host_alloc
+// fails and the caller falls back to ordinary memory; the first "no device"
+// answer is remembered, so GPU-less hosts pay no runtime call per chunk.
+// nxec_host_arena_trim hands free blocks back to the OS.  Ownership lookup is
+// a map of block start -> class under one mutex (a few hundred ns, once per
+// allocate/free).
 #include <hip/hip_runtime.h>
+
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -50,7 +56,10 @@ struct Arena {
   size_t in_use = 0;                      // bytes handed out
   size_t cap = size_t(16) << 30;
   bool disabled = false;
+  bool no_device = false;  // hipHostMalloc said there is no device: stop asking
   Arena() {
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    if (pages > 0 && psz > 0) cap = std::min(cap, static_cast<size_t>(pages) * static_cast<size_t>(psz) / 8);
     if (const char *e = std::getenv("NXEC_HOST_ARENA_MAX")) cap = static_cast<size_t>(std::strtoull(e, nullptr, 10));
     if (cap == 0) disabled = true;
   }
@@ -71,6 +80,7 @@ int nxec_host_alloc(size_t bytes, void **p) {
   const int c = class_of(bytes == 0 ? 1 : bytes);
   Arena &a = arena();
   if (c < 0 || a.disabled) return nxec::set_error(NXEC_ERR_NOMEM, "nxec_host_alloc: %zu bytes not served", bytes);
+  if (a.no_device) return nxec::set_error(NXEC_ERR_NODEV, "nxec_host_alloc: no device");
   const size_t cb = class_bytes(c);
   {
     std::lock_guard<std::mutex> lk(a.mu);
@@ -89,6 +99,7 @@ int nxec_host_alloc(size_t bytes, void **p) {
   if (e != hipSuccess || !blk) {
     (void)hipGetLastError();
     a.pinned -= cb;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) a.no_device = true;
     return nxec::set_error(e == hipErrorNoDevice ? NXEC_ERR_NODEV : NXEC_ERR_NOMEM, "nxec_host_alloc: %s",
                            hipGetErrorString(e));
   }
@@ -122,6 +133,28 @@ int nxec_host_arena_stats(size_t *pinned_bytes, size_t *in_use_bytes) {
   if (pinned_bytes) *pinned_bytes = a.pinned;
   if (in_use_bytes) *in_use_bytes = a.in_use;
   return NXEC_OK;
+}
+
+size_t nxec_host_arena_cap(void) { return arena().cap; }
+
+int nxec_host_arena_trim(size_t keep_bytes) {
+  Arena &a = arena();
+  std::vector<void *> drop;
+  {
+    std::lock_guard<std::mutex> lk(a.mu);
+    for (int c = kClasses - 1; c >= 0 && a.pinned > keep_bytes; c--)  // largest blocks first
+      while (!a.free_list[c].empty() && a.pinned > keep_bytes) {
+        void *p = a.free_list[c].back();
+        a.free_list[c].pop_back();
+        a.owner.erase(p);
+        a.pinned -= class_bytes(c);
+        drop.push_back(p);
+      }
+  }
+  int rc = NXEC_OK;
+  for (void *p : drop)  // unpinning takes a while: outside the lock
+    if (hipHostFree(p) != hipSuccess) rc = nxec::set_error(NXEC_ERR_HIP, "nxec_host_arena_trim: hipHostFree failed");
+  return rc;
 }
 
 }  // extern "C"

@@ -194,7 +194,9 @@ int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 // The agent's form of the fused kernel (nxec_agent_encode_batch): request s
 // reads source j at src_ptrs[s*k + j] and writes output r at dst_ptrs[s*p + r]
 // (device addresses: HBM, or pinned host memory the kernel reads and writes
-// over PCIe), the MD5 of every output to digests + (s*p + r)*16.  scratch: >=
+// over PCIe), the MD5 of every output to digests + (s*p + r)*16 -- with
+// hash_src, of every source too: nh = k + p digests per request, chunk c
+// (sources first) at digests + (s*nh + c)*16.  scratch: >=
 // 2 KiB of device memory, the target of idle lanes' accesses.  Pointer tables
 // and digests may be device-mapped host memory.  Any len > 0 (a partial last
 // step never touches bytes past a chunk's end); every pointer 16-byte aligned.
@@ -206,6 +208,7 @@ struct GatherMd5Args {
   uint8_t *scratch;
   int64_t len, nstripes;
   int32_t k, p;
+  int32_t hash_src;           // sources hashed too
   int32_t stripes_per_group;  // set by launch_gather_md5
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
 };
@@ -216,8 +219,18 @@ int launch_gather_md5(const GatherMd5Args &a, int num_cus, void *stream);
 // all k + p chunks, lens[s] bytes each, digest of chunk c (sources first) at
 // dig_ptrs[s] + c*16.  Bytes up to the next multiple of 16 past lens[s] are
 // readable (and zero for a zero-padded last stripe); outputs are written up
-// to that multiple.  Requests sorted by length, longest first.  Every
-// pointer 16-byte aligned (digests any); tables in device memory.
+// to that multiple.  Every pointer 16-byte aligned (digests any); tables in
+// device memory.
+//
+// Requests are packed into slots (one stripe's worth of code and hash lanes
+// of a workgroup): slot g runs requests slot_reqs[slot_first[g] ..
+// slot_first[g+1]) one after the other, each hash lane finishing one chunk's
+// digest and starting the next chain at a request boundary, so a batch of
+// more requests than the chip has slots (4096 = 256 CUs x 16) runs in one
+// wave of workgroups with every slot's chains about equally long (longest
+// request first into the least loaded slot; plan_files_slots).  Workgroup b
+// owns slots [b*slots_per_group, ...) and runs wg_steps[b] steps of
+// kEncMd5Step bytes (the longest of its slots' totals).
 constexpr int kFilesMd5MaxK = 16;
 struct FilesMd5Args {
   const uint8_t *const *src_ptrs;
@@ -225,12 +238,21 @@ struct FilesMd5Args {
   const int64_t *lens;
   uint8_t *const *dig_ptrs;
   uint8_t *scratch;  // >= 2 KiB of device memory: idle lanes' loads / stores
-  int64_t nstripes;
+  const int32_t *slot_first;  // nslots + 1 entries
+  const int32_t *slot_reqs;
+  const int32_t *wg_steps;    // per workgroup
+  int64_t nslots;
   int32_t k, p;
-  int32_t stripes_per_group;  // set by launch_files_md5
+  int32_t slots_per_group;
+  int32_t max_list;           // longest slot list (LDS request table rows per slot)
   int32_t cached_loads;       // plain loads (default); NXEC_FILES_LOADS=0 streaming (A/B)
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
 };
+// Slot plan for `lens` (descending): fills slot_first / slot_reqs / wg_steps
+// and the args' nslots / slots_per_group / max_list.  NXEC_FILES_PACK=0 gives
+// every request its own slot (one workgroup wave per 4096 requests; A/B).
+void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cus, std::vector<int32_t> &slot_first,
+                      std::vector<int32_t> &slot_reqs, std::vector<int32_t> &wg_steps, FilesMd5Args &a);
 int launch_files_md5(const FilesMd5Args &a, int num_cus, void *stream);
 
 }  // namespace nxec

@@ -17,6 +17,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <system_error>
 #include <thread>
@@ -268,6 +270,24 @@ struct nxec_ctx {
   std::condition_variable agent_cv;
   std::deque<struct AgentJob *> agent_pending;
   bool agent_leader = false;
+  // nxec_encode_host_md5 rounds (zero copy): a leader launches every pending
+  // call in one kernel and hands leadership on at once, so rounds overlap
+  std::mutex dg_mu;
+  std::condition_variable dg_cv;
+  std::deque<struct DigestJob *> dg_pending;
+  bool dg_leader = false;
+  int dg_inflight = 0;
+};
+
+// one nxec_encode_host_md5 call whose buffers are all device-mapped
+struct DigestJob {
+  int len, k, rows;
+  const unsigned char *coeffs;
+  unsigned char *md5_data, *md5_code;
+  std::vector<uintptr_t> in_dv, out_dv;  // device views of the inputs / outputs
+  int rc = NXEC_OK;
+  bool done = false;
+  std::string error;
 };
 
 struct AgentJob {
@@ -357,7 +377,37 @@ int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
   return NXEC_OK;
 }
 
+// Idle slots keep their pinned + device staging for the next call, up to
+// NXEC_SLOT_POOL_MAX bytes per context (default 2 GiB); past it a returned
+// slot gives its buffers back (it keeps its stream), so one large round --
+// e.g. an agent round of many callers -- does not stay pinned for the
+// process's lifetime.
+size_t slot_pool_max() {
+  static const size_t v = [] {
+    const char *e = std::getenv("NXEC_SLOT_POOL_MAX");
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : (size_t(2) << 30);
+  }();
+  return v;
+}
+
 void release_slot(nxec_ctx_t *ctx, Slot *s) {
+  bool drop = false;
+  {
+    std::lock_guard<std::mutex> lk(ctx->slot_mu);
+    size_t pooled = s->cap;
+    for (Slot *f : ctx->free_slots) pooled += f->cap;
+    drop = pooled > slot_pool_max();
+    if (!drop) {
+      ctx->free_slots.push_back(s);
+      return;
+    }
+  }
+  (void)hipStreamSynchronize(s->stream);
+  if (s->h) (void)hipHostFree(s->h);
+  if (s->d) (void)hipFree(s->d);
+  s->h = nullptr;
+  s->d = nullptr;
+  s->cap = 0;
   std::lock_guard<std::mutex> lk(ctx->slot_mu);
   ctx->free_slots.push_back(s);
 }
@@ -1036,7 +1086,7 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
       uprefix.push_back(uprefix.back() + (M + 15) / 16);
     }
   }
-  // fused: requests longest first (a workgroup's first request sets its steps)
+  // fused: requests longest first (the slot planner packs them in this order)
   const bool fused = want_fused && full_aligned && !q_len.empty();
   std::vector<const uint8_t *> f_src;
   std::vector<uint8_t *> f_dst, f_dig;
@@ -1056,6 +1106,11 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
     }
   }
   const std::vector<uint8_t> scratch_pad(fused ? 4096 : 0, 0);  // idle lanes' device line
+  // the fused launch's slots: requests packed so one wave of workgroups runs them all
+  FilesMd5Args fa;
+  std::memset(&fa, 0, sizeof(fa));
+  std::vector<int32_t> slot_first, slot_reqs, wg_steps;
+  if (fused) plan_files_slots(f_len, k, p, ctx->num_cus, slot_first, slot_reqs, wg_steps, fa);
   struct Tab {
     const void *h;
     size_t bytes;
@@ -1065,6 +1120,9 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
                       {f_len.data(), f_len.size() * sizeof(int64_t)},
                       {f_dig.data(), f_dig.size() * sizeof(void *)},
                       {scratch_pad.data(), scratch_pad.size()},
+                      {slot_first.data(), slot_first.size() * sizeof(int32_t)},
+                      {slot_reqs.data(), slot_reqs.size() * sizeof(int32_t)},
+                      {wg_steps.data(), wg_steps.size() * sizeof(int32_t)},
                       {fsrc.data(), fsrc.size() * sizeof(void *)},
                       {fdst.data(), fdst.size() * sizeof(void *)},
                       {pads.data(), pads.size() * sizeof(PadChunks)},
@@ -1086,20 +1144,20 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   for (int i = 0; i < kTabs && !rc; i++)
     if (tabs[i].bytes) std::memcpy(slot->h + off[i], tabs[i].h, tabs[i].bytes);
   if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[kTabs], hipMemcpyHostToDevice, st), "tables H2D");
-  const int T0 = 5;  // the first five tables belong to the fused launch
+  const int T0 = 8;  // the first eight tables belong to the fused launch
   auto dptr = [&](int i) { return slot->d + off[i + T0]; };
   if (fused) {
     if (!rc)
       rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
                              int64_t(pads.size()), pad_blocks, st);
-    FilesMd5Args fa;
-    std::memset(&fa, 0, sizeof(fa));
     fa.src_ptrs = reinterpret_cast<const uint8_t *const *>(slot->d + off[0]);
     fa.dst_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[1]);
     fa.lens = reinterpret_cast<const int64_t *>(slot->d + off[2]);
     fa.dig_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[3]);
     fa.scratch = slot->d + off[4];
-    fa.nstripes = int64_t(f_len.size());
+    fa.slot_first = reinterpret_cast<const int32_t *>(slot->d + off[5]);
+    fa.slot_reqs = reinterpret_cast<const int32_t *>(slot->d + off[6]);
+    fa.wg_steps = reinterpret_cast<const int32_t *>(slot->d + off[7]);
     fa.k = k;
     fa.p = p;
     std::memcpy(fa.coef, prow, size_t(p) * k);
@@ -1134,6 +1192,13 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
 int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
                        const unsigned char *d_chunks, int64_t length, int64_t max_chunk_size, unsigned char *d_object,
                        unsigned char *d_tail, void *stream) {
+  return nxec_decode_object_ex(ctx, n, k, failed, nfailed, d_chunks, max_chunk_size, int64_t(n) * max_chunk_size,
+                               length, max_chunk_size, d_object, d_tail, stream);
+}
+
+int nxec_decode_object_ex(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                          const unsigned char *d_chunks, int64_t chunk_stride, int64_t stripe_stride, int64_t length,
+                          int64_t max_chunk_size, unsigned char *d_object, unsigned char *d_tail, void *stream) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
   int64_t ns = 0, nf = 0, cs_last = 0;
   int rc = nxec_object_layout(n, k, length, max_chunk_size, &ns, &nf, &cs_last);
@@ -1142,16 +1207,19 @@ int nxec_decode_object(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
   const int64_t M = max_chunk_size;
   const bool tail = ns > nf;
   if (!d_chunks || !d_object || (tail && !d_tail)) return set_error(NXEC_ERR_INVALID, "nxec_decode_object: null buffer");
+  if (chunk_stride < M || stripe_stride < int64_t(n) * chunk_stride)
+    return set_error(NXEC_ERR_INVALID, "nxec_decode_object: strides smaller than the chunks");
   hipStream_t st = pick_stream(ctx, stream);
   // full stripes straight into the object: data chunk j of stripe s at s*k*M + j*M
   if (nf > 0) {
-    rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks, M, n * M, d_object, M, k * M, M, nf, st);
+    rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks, chunk_stride, stripe_stride, d_object, M, k * M,
+                                M, nf, st);
     if (rc) return rc;
   }
   if (!tail) return NXEC_OK;
   // last stripe: chunks of cs_last bytes in the same slots; decode to scratch, keep the unpadded bytes
-  rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks + nf * n * M, M, n * M, d_tail, cs_last,
-                              k * cs_last, cs_last, 1, st);
+  rc = nxec_rs_decode_stripes(ctx, n, k, failed, nfailed, d_chunks + nf * stripe_stride, chunk_stride, stripe_stride,
+                              d_tail, cs_last, k * cs_last, cs_last, 1, st);
   if (rc) return rc;
   const int64_t rem = length - nf * k * M;
   return hip_check(hipMemcpyAsync(d_object + nf * k * M, d_tail, rem, hipMemcpyDeviceToDevice, st), "tail copy");
@@ -1255,6 +1323,7 @@ struct AgentBatch {
   Slot *slot = nullptr;
   std::vector<int> reqs;  // request indices staged in this slot (outputs pending)
   size_t out_off = 0, md5_off = 0;
+  int hsrc = 0;  // digests per request: [inputs (hsrc) ][outputs], (hsrc + noutputs) x 16 bytes
   int64_t stride = 0;
   size_t d2h_bytes = 0;  // outputs (+ digests) still to be queued device -> host
   // fused form (k_gather_md5 over pinned memory): the kernel wrote outputs
@@ -1290,7 +1359,7 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
   if (int rc = agent_d2h(ctx, b)) return rc;
   NXEC_HIP(hipStreamSynchronize(b.slot->stream));
   const nxec_agent_req &r0 = reqs[b.reqs[0]];
-  const int no = r0.noutputs;
+  const int no = r0.noutputs, nh = b.hsrc + no;
   HostPool::get().parallel_for(static_cast<int>(b.reqs.size()) * no, [&](int item) {  // scatter the outputs
     const size_t i = static_cast<size_t>(item / no);
     const int o = item % no;
@@ -1299,7 +1368,9 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
       std::memcpy(r.outputs[o], b.slot->h + b.out_off + (i * no + o) * b.stride, cs);
     else if (b.out_pos[static_cast<size_t>(item)] >= 0)
       std::memcpy(r.outputs[o], b.slot->h + b.out_pos[static_cast<size_t>(item)], cs);
-    if (o == 0 && r.md5) std::memcpy(r.md5, b.slot->h + b.md5_off + i * no * 16, size_t(no) * 16);
+    const uint8_t *dg = b.slot->h + b.md5_off + i * size_t(nh) * 16;
+    if (o == 0 && r.md5) std::memcpy(r.md5, dg + size_t(b.hsrc) * 16, size_t(no) * 16);
+    if (o == 0 && r.md5_inputs && b.hsrc) std::memcpy(r.md5_inputs, dg, size_t(b.hsrc) * 16);
   });
   b.reqs.clear();
   return NXEC_OK;
@@ -1311,6 +1382,16 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
 
 static bool agent_trace() {
   static const bool t = std::getenv("NXEC_AGENT_TRACE") != nullptr;
+  return t;
+}
+
+// testing hook: NXEC_TEST_AGENT_THROW=1 makes every round's leader throw
+// before it runs (the round must still complete with an error, no waiter hangs)
+static bool agent_test_throw() {
+  static const bool t = [] {
+    const char *e = std::getenv("NXEC_TEST_AGENT_THROW");
+    return e && e[0] == '1';
+  }();
   return t;
 }
 
@@ -1344,12 +1425,13 @@ static int agent_slot(nxec_ctx_t *ctx, AgentBatch &b, size_t bytes) {
 // 50 GiB/s); with inputs to stage, *taken = false and the caller runs the
 // H2D -> multiply -> D2H form, whose copy engines beat kernel reads of the
 // staging slot when no MD5 chain hides them (pageable: 34 vs 29 GiB/s).
+// hsrc: the inputs are hashed too (RSCode::encode through nxec_encode_host_md5).
 static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const std::vector<int> &ids,
                              int64_t chunk_size, int64_t stride, int64_t batch_bytes, AgentBatch (&slots)[kAgentSlots],
-                             int &cur, bool md5, bool *taken) {
+                             int &cur, bool md5, bool hsrc, bool *taken) {
   *taken = true;
   const nxec_agent_req &r0 = reqs[ids[0]];
-  const int ni = r0.ninputs, no = r0.noutputs;
+  const int ni = r0.ninputs, no = r0.noutputs, nh = (hsrc ? ni : 0) + no;
   const size_t nid = ids.size(), cs = size_t(chunk_size);
   std::vector<uintptr_t> in_dv(nid * ni), out_dv(nid * no);  // 0: not mapped
   const auto tc0 = std::chrono::steady_clock::now();
@@ -1380,7 +1462,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       int64_t n_st = 0;
       for (int j = 0; j < ni; j++) n_st += in_dv[last * ni + j] == 0;
       for (int o = 0; o < no; o++) n_st += out_dv[last * no + o] == 0;
-      const int64_t need = n_st * stride + (md5 ? int64_t(no) * 16 : 0) + (int64_t(ni) + no) * 8;
+      const int64_t need = n_st * stride + (md5 ? int64_t(nh) * 16 : 0) + (int64_t(ni) + no) * 8;
       if (last > first && staged + need > batch_bytes) break;
       staged += need;
       last++;
@@ -1407,8 +1489,9 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       if (!out_dv[first * no + q]) b.out_pos[q] = pos, pos += stride;
     b.fused = true;
     b.stride = stride;
+    b.hsrc = hsrc ? ni : 0;
     b.md5_off = size_t(pos);
-    const size_t tab_off = b.md5_off + (md5 ? nb * no * 16 : 0);
+    const size_t tab_off = b.md5_off + (md5 ? nb * size_t(nh) * 16 : 0);
     uint64_t *src_tab = reinterpret_cast<uint64_t *>(b.slot->h + tab_off);
     uint64_t *dst_tab = src_tab + nb * ni;
     HostPool::get().parallel_for(static_cast<int>(nb * (ni + no)), [&](int item) {
@@ -1453,6 +1536,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
     ga.nstripes = int64_t(nb);
     ga.k = ni;
     ga.p = no;
+    ga.hash_src = hsrc ? 1 : 0;
     std::memcpy(ga.coef, r0.matrix, size_t(no) * ni);
     if ((rc = launch_gather_md5(ga, ctx->num_cus, b.slot->stream))) break;
     b.d2h_bytes = 0;
@@ -1472,7 +1556,8 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
   std::map<std::string, std::vector<int>> groups;
   for (int i = 0; i < nreqs; i++) {
     const nxec_agent_req &r = reqs[i];
-    std::string key(reinterpret_cast<const char *>(&r.ninputs), sizeof(int));
+    std::string key(1, r.md5_inputs ? 'S' : '-');  // inputs hashed: its own kernel form
+    key.append(reinterpret_cast<const char *>(&r.ninputs), sizeof(int));
     key.append(reinterpret_cast<const char *>(&r.noutputs), sizeof(int));
     key.append(reinterpret_cast<const char *>(r.matrix), size_t(r.ninputs) * r.noutputs);
     groups[key].push_back(i);
@@ -1499,15 +1584,18 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
     const std::vector<int> &ids = kv.second;
     const nxec_agent_req &r0 = reqs[ids[0]];
     const int ni = r0.ninputs, no = r0.noutputs;
-    bool group_md5 = false;
+    const bool hsrc = r0.md5_inputs != nullptr;  // the whole group (grouping key)
+    bool group_md5 = hsrc;
     for (int id : ids) group_md5 |= reqs[id].md5 != nullptr;
+    const int nh = (hsrc ? ni : 0) + no;
     if (fused_env && host_direct && ni <= kGatherMd5MaxK && no <= kMaxRowsPerPass) {
       bool taken = false;
-      if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur, group_md5, &taken)))
+      if ((rc = agent_fused_group(ctx, reqs, ids, chunk_size, stride, batch_bytes, slots, cur, group_md5, hsrc,
+                                  &taken)))
         break;
       if (taken) continue;
     }
-    const int64_t per = (int64_t(ni) + no) * stride + int64_t(no) * 16;
+    const int64_t per = (int64_t(ni) + no) * stride + int64_t(nh) * 16;
     const int64_t B = std::max<int64_t>(1, std::min<int64_t>(int64_t(ids.size()), batch_bytes / per));
     const size_t slot_bytes = size_t(B * per);
     for (size_t first = 0; first < ids.size() && rc == NXEC_OK; first += B) {
@@ -1523,6 +1611,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
       b.out_off = in_bytes;
       b.md5_off = in_bytes + size_t(nb) * no * stride;
       b.fused = false;
+      b.hsrc = hsrc ? ni : 0;
       HostPool::get().parallel_for(static_cast<int>(nb) * ni, [&](int item) {  // gather into pinned staging
         const int64_t i = item / ni;
         const int j = item % ni;
@@ -1538,18 +1627,20 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
       }
       hipStream_t st = b.slot->stream;
       uint8_t *d_in = b.slot->d, *d_out = b.slot->d + b.out_off, *d_md5 = b.slot->d + b.md5_off;
-      bool any_md5 = false;
+      bool any_md5 = hsrc;
       for (int64_t i = 0; i < nb; i++) any_md5 |= reqs[ids[first + i]].md5 != nullptr;
       if ((rc = hip_check(hipMemcpyAsync(d_in, b.slot->h, in_bytes, hipMemcpyHostToDevice, st), "agent H2D"))) break;
       // CodingUtils::encode (container_manager.cc:251, agent.cc:339) for the whole batch
       rc = nxec_stripes_mul(ctx, no, ni, r0.matrix, d_in, nullptr, stride, ni * stride, d_out, nullptr, stride,
                             no * stride, nullptr, chunk_size, nb, st);
       if (rc) break;
-      if (any_md5) {  // Chunk::computeMD5 of the outputs (agent.cc:342)
-        const Md5Region reg{d_out, stride, no * stride, chunk_size, nb, d_md5, int64_t(no) * 16, no};
-        if ((rc = launch_md5(&reg, 1, st))) break;
+      if (any_md5) {  // Chunk::computeMD5 of the outputs (agent.cc:342), and of the inputs for hsrc
+        const int64_t ds = int64_t(nh) * 16;
+        const Md5Region reg[2] = {{d_out, stride, no * stride, chunk_size, nb, d_md5 + (hsrc ? ni * 16 : 0), ds, no},
+                                  {d_in, stride, ni * stride, chunk_size, nb, d_md5, ds, ni}};
+        if ((rc = launch_md5(reg, hsrc ? 2 : 1, st))) break;
       }
-      b.d2h_bytes = size_t(nb) * (no * stride + (any_md5 ? no * 16 : 0));
+      b.d2h_bytes = size_t(nb) * (no * stride + (any_md5 ? nh * 16 : 0));
       if ((rc = agent_d2h(ctx, other))) break;  // the previous batch's D2H, behind this batch's H2D
     }
     if (rc) break;
@@ -1572,7 +1663,9 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
 // taking every queued job of the same chunk size, and runs them as ONE set of
 // batches (one MD5 launch per batch covers all callers' outputs, so the ~10 ms
 // MD5 chain of a 1 MiB chunk is paid once per round, not once per call).
-// Rounds use larger staging (>= 512 MiB per slot) than a lone call.
+// A round stages at most the smallest batch_bytes its callers asked for;
+// when none asked, 512 MiB per slot for a merged round (4 pageable callers:
+// 20 GiB/s at 1 GiB, 26 at 512 MiB) and 256 MiB for a lone call.
 // NXEC_AGENT_AGGREGATE=0 runs every call on its own.
 extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nreqs, int64_t chunk_size,
                                        int64_t batch_bytes) {
@@ -1616,19 +1709,27 @@ extern "C" int nxec_agent_encode_batch(nxec_ctx_t *ctx, const nxec_agent_req *re
       }
     }
     lk.unlock();
-    std::vector<nxec_agent_req> merged;
-    int64_t bb = int64_t(512) << 20;  // fused form, 4 pageable callers: 20 GiB/s at 1 GiB, 26 at 512 MiB
-    for (AgentJob *j : round) {
-      merged.insert(merged.end(), j->reqs, j->reqs + j->nreqs);
-      bb = std::max(bb, j->batch_bytes);
-    }
-    if (round.size() == 1) bb = round[0]->batch_bytes;  // a lone call keeps its own staging bound
     // (overlapping rounds -- leadership handed on once a round's batches are
     // queued -- measured worse: many small rounds, each paying a whole MD5
     // chain, and two rounds' gathers sharing the host pool; 16 callers 5-11
     // vs 27-29 GiB/s, profiles/r02_agent_nt_staging.log)
-    const int rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
-    const std::string err = rc ? g_last_error : std::string();
+    int rc = NXEC_OK;
+    std::string err;
+    try {  // whatever happens, the round's jobs finish and leadership is released
+      std::vector<nxec_agent_req> merged;
+      int64_t bb = 0;  // the smallest staging bound any caller of the round asked for
+      for (AgentJob *j : round) {
+        merged.insert(merged.end(), j->reqs, j->reqs + j->nreqs);
+        if (j->batch_bytes > 0) bb = bb > 0 ? std::min(bb, j->batch_bytes) : j->batch_bytes;
+      }
+      if (bb <= 0 && round.size() > 1) bb = int64_t(512) << 20;
+      if (agent_test_throw()) throw std::bad_alloc();
+      rc = agent_encode_impl(ctx, merged.data(), static_cast<int>(merged.size()), cs0, bb);
+      if (rc) err = g_last_error;
+    } catch (const std::exception &e) {
+      rc = set_error(NXEC_ERR_NOMEM, "nxec_agent_encode_batch: %s", e.what());
+      err = g_last_error;
+    }
     lk.lock();
     for (AgentJob *j : round) {
       j->rc = rc;
@@ -2300,6 +2401,205 @@ int nxec_encode_host(int len, int k, int rows, const unsigned char *coeffs, cons
   return nxec_encode_host_ex(len, k, rows, coeffs, data, coding, nullptr, nullptr);
 }
 
+}  // extern "C"
+
+namespace {
+
+int digest_rounds_max() {
+  static const int v = [] {
+    const char *e = std::getenv("NXEC_DIGEST_ROUNDS");
+    return e ? std::max(1, std::atoi(e)) : 4;
+  }();
+  return v;
+}
+
+// One round of zero-copy digest calls: per group of equal (len, k, rows,
+// inputs hashed, matrix) one k_gather_md5 launch over pointer tables in a
+// pinned slot (device-mapped: no H2D), digests written back into the slot.
+// Returns after the launches are queued; `wait` finishes the round.
+struct DigestRound {
+  struct Group {
+    std::vector<DigestJob *> jobs;
+    Slot *slot = nullptr;
+    size_t md5_off = 0;
+    int nh = 0;
+    bool hsrc = false;
+  };
+  std::vector<Group> groups;
+};
+
+int digest_round_launch(nxec_ctx_t *ctx, const std::vector<DigestJob *> &jobs, DigestRound &round) {
+  std::map<std::string, size_t> key_of;
+  for (DigestJob *j : jobs) {
+    std::string key(reinterpret_cast<const char *>(&j->len), sizeof(int));
+    key.append(reinterpret_cast<const char *>(&j->k), sizeof(int));
+    key.append(reinterpret_cast<const char *>(&j->rows), sizeof(int));
+    key.append(1, j->md5_data ? 'S' : '-');
+    key.append(reinterpret_cast<const char *>(j->coeffs), size_t(j->rows) * j->k);
+    auto it = key_of.find(key);
+    if (it == key_of.end()) {
+      it = key_of.emplace(key, round.groups.size()).first;
+      round.groups.emplace_back();
+    }
+    round.groups[it->second].jobs.push_back(j);
+  }
+  for (DigestRound::Group &g : round.groups) {
+    const DigestJob &j0 = *g.jobs[0];
+    const int k = j0.k, p = j0.rows;
+    g.hsrc = j0.md5_data != nullptr;
+    g.nh = (g.hsrc ? k : 0) + p;
+    const size_t nb = g.jobs.size();
+    const size_t tab_bytes = nb * size_t(k + p) * 8;
+    g.md5_off = (tab_bytes + 255) / 256 * 256;
+    const size_t need = std::max<size_t>(g.md5_off + nb * size_t(g.nh) * 16, 4096);
+    if (int rc = acquire_slot(ctx, need, &g.slot)) return rc;
+    uint8_t *hv = static_cast<uint8_t *>(host_device_view(g.slot->h));
+    if (!hv) return set_error(NXEC_ERR_HIP, "encode_host_md5: staging slot is not device-mapped");
+    uint64_t *src_tab = reinterpret_cast<uint64_t *>(g.slot->h);
+    uint64_t *dst_tab = src_tab + nb * k;
+    for (size_t i = 0; i < nb; i++) {
+      for (int q = 0; q < k; q++) src_tab[i * k + q] = g.jobs[i]->in_dv[q];
+      for (int r = 0; r < p; r++) dst_tab[i * p + r] = g.jobs[i]->out_dv[r];
+    }
+    GatherMd5Args ga;
+    std::memset(&ga, 0, sizeof(ga));
+    ga.src_ptrs = reinterpret_cast<const uint8_t *const *>(hv);
+    ga.dst_ptrs = reinterpret_cast<uint8_t *const *>(hv + nb * k * 8);
+    ga.digests = hv + g.md5_off;
+    ga.scratch = g.slot->d;
+    ga.len = j0.len;
+    ga.nstripes = int64_t(nb);
+    ga.k = k;
+    ga.p = p;
+    ga.hash_src = g.hsrc ? 1 : 0;
+    std::memcpy(ga.coef, j0.coeffs, size_t(p) * k);
+    if (int rc = launch_gather_md5(ga, ctx->num_cus, g.slot->stream)) return rc;
+  }
+  return NXEC_OK;
+}
+
+int digest_round_wait(nxec_ctx_t *ctx, DigestRound &round, int rc) {
+  for (DigestRound::Group &g : round.groups) {
+    if (!g.slot) continue;
+    const hipError_t e = hipStreamSynchronize(g.slot->stream);
+    if (!rc) rc = hip_check(e, "encode_host_md5 sync");
+    if (!rc)
+      for (size_t i = 0; i < g.jobs.size(); i++) {
+        const uint8_t *dg = g.slot->h + g.md5_off + i * size_t(g.nh) * 16;
+        DigestJob &j = *g.jobs[i];
+        if (j.md5_data) std::memcpy(j.md5_data, dg, size_t(j.k) * 16);
+        if (j.md5_code) std::memcpy(j.md5_code, dg + (g.hsrc ? size_t(j.k) * 16 : 0), size_t(j.rows) * 16);
+      }
+    release_slot(ctx, g.slot);
+    g.slot = nullptr;
+  }
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+// nxec_encode_host + digests.  Calls whose chunks are all device-mapped (arena
+// Chunks: RSCode::encode's own stripe) go through digest rounds: whichever
+// waiting caller finds no round being launched takes every pending call,
+// launches them as one k_gather_md5 pass per shape over pointer tables (zero
+// copy: no H2D, no D2H) and hands leadership on right after the launch, so
+// the next round starts while this one's MD5 chains (~10 ms per MiB on one
+// lane, whatever the round's size) run -- up to NXEC_DIGEST_ROUNDS (4) rounds
+// in flight.  (The agent service's rounds, below, finish before the next one
+// starts: their host gathers of pageable buffers are the bottleneck there.)
+// Other calls (pageable or misaligned buffers, k > 16, rows > 4) take the
+// agent service's staged form as one request.
+int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                         unsigned char *const *coding, unsigned char *md5_data, unsigned char *md5_code) {
+  if (len < 0 || k < 1 || k > NXEC_MAX_K || rows < 1 || rows > NXEC_MAX_N || !coeffs || !data || !coding)
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_host_md5: invalid arguments");
+  if (!md5_data && !md5_code) return nxec_encode_host(len, k, rows, coeffs, data, coding);
+  if (len == 0) {  // RFC 1321 digest of the empty message
+    static const unsigned char empty[16] = {0xd4, 0x1d, 0x8c, 0xd9, 0x8f, 0x00, 0xb2, 0x04,
+                                            0xe9, 0x80, 0x09, 0x98, 0xec, 0xf8, 0x42, 0x7e};
+    for (int j = 0; md5_data && j < k; j++) std::memcpy(md5_data + 16 * j, empty, 16);
+    for (int r = 0; md5_code && r < rows; r++) std::memcpy(md5_code + 16 * r, empty, 16);
+    return NXEC_OK;
+  }
+  nxec_ctx_t *ctx = nullptr;
+  int rc = default_ctx(&ctx);
+  if (rc) return rc;
+  if ((rc = ensure_device(ctx->device))) return rc;
+  DigestJob job;
+  job.len = len;
+  job.k = k;
+  job.rows = rows;
+  job.coeffs = coeffs;
+  job.md5_data = md5_data;
+  job.md5_code = md5_code;
+  static const bool rounds_env = [] {
+    const char *e = std::getenv("NXEC_DIGEST_ROUNDS");
+    return !(e && e[0] == '0');
+  }();
+  bool mapped = rounds_env && k <= kGatherMd5MaxK && rows <= kMaxRowsPerPass;
+  for (int j = 0; j < k && mapped; j++) {
+    void *dv = aligned16(data[j]) ? host_device_view_range(data[j], size_t(len)) : nullptr;
+    mapped = dv != nullptr;
+    job.in_dv.push_back(reinterpret_cast<uintptr_t>(dv));
+  }
+  for (int r = 0; r < rows && mapped; r++) {
+    void *dv = aligned16(coding[r]) ? host_device_view_range(coding[r], size_t(len)) : nullptr;
+    mapped = dv != nullptr;
+    job.out_dv.push_back(reinterpret_cast<uintptr_t>(dv));
+  }
+  if (!mapped) {
+    nxec_agent_req r;
+    r.ninputs = k;
+    r.noutputs = rows;
+    r.matrix = coeffs;
+    r.inputs = data;
+    r.outputs = coding;
+    r.md5 = md5_code;
+    r.md5_inputs = md5_data;
+    return nxec_agent_encode_batch(ctx, &r, 1, len, 0);
+  }
+  std::unique_lock<std::mutex> lk(ctx->dg_mu);
+  ctx->dg_pending.push_back(&job);
+  while (!job.done) {
+    if (ctx->dg_leader || ctx->dg_pending.empty() || ctx->dg_inflight >= digest_rounds_max()) {
+      ctx->dg_cv.wait(lk);
+      continue;
+    }
+    ctx->dg_leader = true;
+    ctx->dg_inflight++;
+    std::vector<DigestJob *> jobs(ctx->dg_pending.begin(), ctx->dg_pending.end());
+    ctx->dg_pending.clear();
+    lk.unlock();
+    DigestRound round;
+    int rrc = NXEC_OK;
+    std::string err;
+    try {
+      rrc = digest_round_launch(ctx, jobs, round);
+    } catch (const std::exception &e) {
+      rrc = set_error(NXEC_ERR_NOMEM, "nxec_encode_host_md5: %s", e.what());
+    }
+    lk.lock();
+    ctx->dg_leader = false;  // the next round may launch while this one runs
+    ctx->dg_cv.notify_all();
+    lk.unlock();
+    rrc = digest_round_wait(ctx, round, rrc);
+    if (rrc) err = g_last_error;
+    lk.lock();
+    for (DigestJob *j : jobs) {
+      j->rc = rrc;
+      j->error = err;
+      j->done = true;
+    }
+    ctx->dg_inflight--;
+    ctx->dg_cv.notify_all();
+  }
+  lk.unlock();
+  if (job.rc != NXEC_OK) g_last_error = job.error;
+  return job.rc;
+}
+
 int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gftbls, const unsigned char *const *data,
                                unsigned char *const *coding) {
   if (!gftbls || k < 1 || rows < 1) return set_error(NXEC_ERR_INVALID, "nxec_ec_encode_data: invalid arguments");
@@ -2309,13 +2609,82 @@ int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gf
   return nxec_encode_host(len, k, rows, coeffs.data(), data, coding);
 }
 
+}  // extern "C"
+
+namespace {
+
+// The plainest path to the GPU, for the retry of the void drop-in: a new
+// context (its own stream and staging), inputs copied into pinned staging, one
+// H2D, the multiply, one D2H, synchronise, copy out.  No zero copy, no
+// pipelining, nothing shared with the context whose call failed.
+int encode_host_fresh_staged(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
+                             unsigned char *const *coding) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  (void)hipGetLastError();
+  nxec_ctx_t *ctx = nullptr;
+  int rc = nxec_ctx_create(dev, &ctx);
+  if (rc) return rc;
+  const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;
+  Slot *slot = nullptr;
+  rc = acquire_slot(ctx, static_cast<size_t>(stride) * (k + rows), &slot);
+  if (!rc) {
+    for (int j = 0; j < k; j++) std::memcpy(slot->h + j * stride, data[j], static_cast<size_t>(len));
+    rc = hip_check(hipMemcpyAsync(slot->d, slot->h, static_cast<size_t>(stride) * k, hipMemcpyHostToDevice, slot->stream),
+                   "retry H2D");
+    std::vector<int32_t> dst(rows);
+    for (int r = 0; r < rows; r++) dst[r] = k + r;
+    if (!rc)
+      rc = nxec_stripes_mul(ctx, rows, k, coeffs, slot->d, nullptr, stride, 0, slot->d, dst.data(), stride, 0, nullptr,
+                            len, 1, slot->stream);
+    if (!rc)
+      rc = hip_check(hipMemcpyAsync(slot->h + stride * k, slot->d + stride * k, static_cast<size_t>(stride) * rows,
+                                    hipMemcpyDeviceToHost, slot->stream),
+                     "retry D2H");
+    const hipError_t e = hipStreamSynchronize(slot->stream);
+    if (!rc) rc = hip_check(e, "retry sync");
+    if (!rc)
+      for (int r = 0; r < rows; r++) std::memcpy(coding[r], slot->h + (k + r) * stride, static_cast<size_t>(len));
+    release_slot(ctx, slot);
+  }
+  nxec_ctx_destroy(ctx);
+  return rc;
+}
+
+// testing hook: NXEC_TEST_FAIL_ENCODE=1 makes the first attempt of every
+// nxec_ec_encode_data call fail as a device error would (no work done)
+bool test_fail_first_attempt() {
+  static const bool t = [] {
+    const char *e = std::getenv("NXEC_TEST_FAIL_ENCODE");
+    return e && e[0] == '1';
+  }();
+  return t;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ISA-L's ec_encode_data has no error channel (erasure_code.h:98, rs.cc:89),
+// so a failed device pass is retried once on a fresh context through the
+// staged path (a transient error -- a busy queue, a lost stream -- does not
+// take the proxy and its background repair thread down); only when that fails
+// too does the process stop rather than return undefined parity.
 void nxec_ec_encode_data(int len, int k, int rows, unsigned char *gftbls, unsigned char **data,
                          unsigned char **coding) {
-  int rc = nxec_ec_encode_data_status(len, k, rows, gftbls, data, coding);
-  if (rc != NXEC_OK) {
-    std::fprintf(stderr, "nxec_ec_encode_data failed (%d): %s\n", rc, nxec_last_error());
-    std::abort();
+  int rc = test_fail_first_attempt() ? set_error(NXEC_ERR_HIP, "injected device error (NXEC_TEST_FAIL_ENCODE)")
+                                     : nxec_ec_encode_data_status(len, k, rows, gftbls, data, coding);
+  if (rc == NXEC_OK) return;
+  if (rc != NXEC_ERR_INVALID) {
+    std::fprintf(stderr, "nxec_ec_encode_data failed (%d): %s; retrying once on a fresh context (staged)\n", rc,
+                 nxec_last_error());
+    std::vector<uint8_t> coeffs(static_cast<size_t>(rows) * k);
+    for (size_t i = 0; i < coeffs.size(); i++) coeffs[i] = gftbls[32 * i + 1];
+    rc = encode_host_fresh_staged(len, k, rows, coeffs.data(), data, coding);
+    if (rc == NXEC_OK) return;
   }
+  std::fprintf(stderr, "nxec_ec_encode_data failed (%d): %s\n", rc, nxec_last_error());
+  std::abort();
 }
 
 // ---- plumbing ----
@@ -2384,6 +2753,12 @@ int nxec_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes, void *stream) 
 }
 int nxec_memset(void *d_dst, int value, size_t bytes, void *stream) {
   NXEC_HIP(hipMemsetAsync(d_dst, value, bytes, static_cast<hipStream_t>(stream)));
+  return NXEC_OK;
+}
+int nxec_memset2d(void *d_dst, size_t pitch, int value, size_t width, size_t height, void *stream) {
+  if (!d_dst || width > pitch) return set_error(NXEC_ERR_INVALID, "nxec_memset2d: invalid arguments");
+  if (!width || !height) return NXEC_OK;
+  NXEC_HIP(hipMemset2DAsync(d_dst, pitch, value, width, height, static_cast<hipStream_t>(stream)));
   return NXEC_OK;
 }
 int nxec_stream_create(void **stream) {

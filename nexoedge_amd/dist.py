@@ -73,6 +73,17 @@ class RankGroup:
     def max(self, x: float) -> float:
         return self._reduce(x, "MAX")
 
+    def gather(self, x: float) -> list:
+        """Every rank's x, in rank order, on every rank."""
+        if self._dist is None:
+            return [float(x)]
+        import torch
+
+        t = torch.zeros(self.world, dtype=torch.float64)
+        t[self.rank] = float(x)
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
+        return [float(v) for v in t.tolist()]
+
     def sum(self, x: float) -> float:
         return self._reduce(x, "SUM")
 

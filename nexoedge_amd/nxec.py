@@ -144,6 +144,31 @@ def encode_host(coeffs: np.ndarray, data: Sequence[np.ndarray]) -> list:
     return outs
 
 
+def encode_host_md5(coeffs: np.ndarray, data: Sequence, outs: Optional[Sequence] = None, hash_inputs: bool = True):
+    """nxec_encode_host_md5: encode_host plus the MD5 of the inputs (when
+    hash_inputs) and outputs from the same GPU pass.  data / outs may be numpy
+    arrays or (address, length) pairs of host memory (e.g. arena blocks).
+    Returns (outputs, input digests (k x 16) or None, output digests (rows x 16))."""
+    c = np.ascontiguousarray(coeffs, dtype=np.uint8)
+    rows, k = c.shape
+
+    def addr(a):
+        return (int(a[0]), int(a[1])) if isinstance(a, tuple) else (a.ctypes.data, len(a))
+
+    ins = [a if isinstance(a, tuple) else np.ascontiguousarray(a, dtype=np.uint8) for a in data]
+    n = addr(ins[0])[1] if ins else 0
+    if outs is None:
+        outs = [np.zeros(n, dtype=np.uint8) for _ in range(rows)]
+    md5_in = np.zeros((k, 16), dtype=np.uint8) if hash_inputs else None
+    md5_out = np.zeros((rows, 16), dtype=np.uint8)
+    inp = (C.c_void_p * k)(*[addr(d)[0] for d in ins])
+    outp = (C.c_void_p * rows)(*[addr(o)[0] for o in outs])
+    check(lib.nxec_encode_host_md5(n, k, rows, _u8(c), inp, outp,
+                                   _u8(md5_in) if md5_in is not None else None, _u8(md5_out)),
+          "nxec_encode_host_md5")
+    return outs, md5_in, md5_out
+
+
 def ec_encode_data(gftbls: np.ndarray, k: int, rows: int, data: Sequence[np.ndarray]) -> list:
     """Drop-in ISA-L signature: coefficients come from 32-byte tables."""
     t = np.ascontiguousarray(gftbls, dtype=np.uint8)
@@ -193,6 +218,35 @@ def device_sync() -> None:
     check(lib.nxec_device_sync(), "nxec_device_sync")
 
 
+def bind_thread_numa(device: int) -> int:
+    """Binds the calling thread (and threads it starts later) to the CPUs of
+    the NUMA node of GPU `device` (nxec_bind_thread_to_device); returns the
+    node, -1 when unknown (affinity unchanged)."""
+    node = C.c_int(-1)
+    check(lib.nxec_bind_thread_to_device(device, C.byref(node)), "nxec_bind_thread_to_device")
+    return node.value
+
+
+def pci_numa_node(bus_id: str) -> int:
+    node = C.c_int(-1)
+    check(lib.nxec_pci_numa_node(bus_id.encode(), C.byref(node)), "nxec_pci_numa_node")
+    return node.value
+
+
+def numa_node_cpus(node: int) -> list:
+    cnt = C.c_int(0)
+    check(lib.nxec_numa_node_cpus(node, None, 0, C.byref(cnt)), "nxec_numa_node_cpus")
+    arr = (C.c_int * max(cnt.value, 1))()
+    check(lib.nxec_numa_node_cpus(node, arr, cnt.value, C.byref(cnt)), "nxec_numa_node_cpus")
+    return list(arr[:cnt.value])
+
+
+def bind_thread_pci(bus_id: str) -> int:
+    node = C.c_int(-1)
+    check(lib.nxec_bind_thread_to_pci(bus_id.encode(), C.byref(node)), "nxec_bind_thread_to_pci")
+    return node.value
+
+
 class DeviceBuffer:
     """Raw device allocation (hipMalloc) with host copy helpers."""
 
@@ -230,6 +284,11 @@ class DeviceBuffer:
         n = self.nbytes - offset if nbytes is None else nbytes
         check(lib.nxec_memset(self.addr(offset), value, n, stream), "memset")
         check(lib.nxec_stream_sync(stream), "sync")
+
+    def memset2d(self, value: int, offset: int, pitch: int, width: int, height: int, stream=None) -> None:
+        """Asynchronous: `height` rows of `width` bytes, `pitch` apart, from `offset` (hipMemset2DAsync)."""
+        assert offset + (height - 1) * pitch + width <= self.nbytes if height else True
+        check(lib.nxec_memset2d(self.addr(offset), pitch, value, width, height, stream), "memset2d")
 
     def copy_within(self, dst_offset: int, src_offset: int, nbytes: int, stream=None) -> None:
         """Asynchronous device-to-device copy inside this buffer (hipMemcpyAsync)."""
@@ -422,6 +481,13 @@ class Context:
                                      max_chunk_size, C.c_void_p(int(obj)), C.c_void_p(int(tail) if tail else None),
                                      stream), "nxec_decode_object")
 
+    def decode_object_ex(self, n: int, k: int, failed: Sequence[int], chunks: int, chunk_stride: int,
+                         stripe_stride: int, length: int, max_chunk_size: int, obj: int, tail=None, stream=None) -> None:
+        f, fp = _i32(failed)
+        check(lib.nxec_decode_object_ex(C.c_void_p(self.ptr), n, k, fp, len(failed), C.c_void_p(int(chunks)),
+                                        chunk_stride, stripe_stride, length, max_chunk_size, C.c_void_p(int(obj)),
+                                        C.c_void_p(int(tail) if tail else None), stream), "nxec_decode_object_ex")
+
     def decode_object_verify(self, n: int, k: int, failed: Sequence[int], chunks: int, length: int,
                              max_chunk_size: int, md5: int, obj: int, tail, ok: int, nbad=None, stream=None) -> None:
         """nxec_decode_object_verify: decode_object + MD5 check of every chunk read (ok [ns][n] bytes)."""
@@ -434,16 +500,20 @@ class Context:
 
     def agent_encode_batch(self, reqs, chunk_size: int, batch_bytes: int = 0) -> None:
         """nxec_agent_encode_batch: reqs = [(matrix (no x ni), inputs [ni arrays], outputs [no arrays],
-        md5 (no x 16 uint8 array) or None)], host numpy buffers of chunk_size bytes."""
+        md5 (no x 16 uint8 array) or None[, md5_inputs (ni x 16) or None])], host numpy buffers of
+        chunk_size bytes."""
         keep = []
         arr = (AgentReq * max(len(reqs), 1))()
-        for i, (m, ins, outs, md5) in enumerate(reqs):
+        for i, req in enumerate(reqs):
+            m, ins, outs, md5 = req[:4]
+            md5_in = req[4] if len(req) > 4 else None
             m = np.ascontiguousarray(m, dtype=np.uint8)
             ip = (C.c_void_p * len(ins))(*[a.ctypes.data for a in ins])
             op = (C.c_void_p * len(outs))(*[a.ctypes.data for a in outs])
             keep += [m, ip, op]
             arr[i] = AgentReq(len(ins), len(outs), m.ctypes.data, C.cast(ip, C.c_void_p), C.cast(op, C.c_void_p),
-                                   md5.ctypes.data if md5 is not None else None)
+                              md5.ctypes.data if md5 is not None else None,
+                              md5_in.ctypes.data if md5_in is not None else None)
         check(lib.nxec_agent_encode_batch(C.c_void_p(self.ptr), arr, len(reqs), chunk_size, batch_bytes),
               "nxec_agent_encode_batch")
 

@@ -120,3 +120,76 @@ def test_batch_layout_policy():
         for fl in (0, 1):
             cs, ss = nxec.batch_layout(n, ln, fl)
             assert cs >= ln and ss >= n * cs and cs % 16 == 0 and ss % 16 == 0
+
+
+VOID_FORM = r"""
+import ctypes, sys
+sys.path.insert(0, {root!r})
+from nexoedge_amd import _lib
+lib = _lib.lib
+k, rows, n = 2, 1, 64
+t = (ctypes.c_ubyte * (32 * k * rows))()
+lib.nxec_ec_init_tables(k, rows, (ctypes.c_ubyte * 2)(1, 1), t)
+bufs = [(ctypes.c_ubyte * n)() for _ in range(k + rows)]
+data = (ctypes.c_void_p * k)(*[ctypes.addressof(b) for b in bufs[:k]])
+code = (ctypes.c_void_p * rows)(*[ctypes.addressof(b) for b in bufs[k:]])
+lib.nxec_ec_encode_data(n, k, rows, t, data, code)
+print("RETURNED", flush=True)
+"""
+
+
+def test_void_form_retries_then_aborts_without_a_device():
+    """Option A: nxec_ec_encode_data keeps ISA-L's void
+    signature (erasure_code.h:98).  A device error is retried once on a fresh
+    context through the staged path; only when that fails too (here: no
+    device at all) does it abort -- never return undefined parity.  The
+    _status form reports the same failure as a return code."""
+    import signal
+    import sys
+
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="", ROCR_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-c", VOID_FORM.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == -signal.SIGABRT, (r.returncode, r.stderr[-2000:])
+    assert "retrying once on a fresh context" in r.stderr and "RETURNED" not in r.stdout
+    # bad arguments are not retried (they cannot succeed)
+    bad = VOID_FORM.replace("lib.nxec_ec_encode_data(n, k, rows", "lib.nxec_ec_encode_data(-1, k, rows")
+    r = subprocess.run([sys.executable, "-c", bad.format(root=ROOT)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == -signal.SIGABRT and "retrying" not in r.stderr
+
+
+def test_digest_table_is_per_thread_and_taken_once():
+    """include/nxec.h §6b: a digest noted by a coding call is found only by
+    the same thread, only for the same (pointer, length), and only once."""
+    import threading
+
+    import numpy as np
+
+    buf = np.zeros(4096, dtype=np.uint8)
+    d = np.arange(16, dtype=np.uint8)
+    got = np.zeros(16, dtype=np.uint8)
+    lib = _lib.lib
+    lib.nxec_digest_clear()
+    assert lib.nxec_digest_note(buf.ctypes.data, 4096, d.ctypes.data) == 0
+    seen = []
+    th = threading.Thread(target=lambda: seen.append(lib.nxec_digest_take(buf.ctypes.data, 4096, got.ctypes.data)))
+    th.start()
+    th.join()
+    assert seen == [0]  # another thread's table is empty
+    assert lib.nxec_digest_take(buf.ctypes.data, 4096, got.ctypes.data) == 1 and (got == d).all()
+    assert lib.nxec_digest_take(buf.ctypes.data, 4096, got.ctypes.data) == 0
+    lib.nxec_digest_note(buf.ctypes.data, 4096, d.ctypes.data)
+    lib.nxec_digest_forget(buf.ctypes.data)
+    assert lib.nxec_digest_take(buf.ctypes.data, 4096, got.ctypes.data) == 0
+    assert lib.nxec_chunk_md5_mode() in (0, 1, 2)
+
+
+def test_arena_bound_defaults_to_a_fraction_of_ram():
+    """the pinned arena's default bound is an eighth of physical
+    memory, at most 16 GiB (NXEC_HOST_ARENA_MAX overrides)."""
+    if "NXEC_HOST_ARENA_MAX" in os.environ:
+        pytest.skip("bound set explicitly")
+    ram = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGESIZE")
+    assert _lib.lib.nxec_host_arena_cap() == min(16 << 30, ram // 8)
+    assert _lib.lib.nxec_host_arena_trim(0) == 0

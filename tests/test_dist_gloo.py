@@ -38,7 +38,8 @@ g.barrier()
 t = 0.010 * (g.rank + 1)          # pretend rank r took (r+1)*10 ms
 mx = g.max(t)
 tot = g.sum(hi - lo)
-print(f"rank={{g.rank}} world={{g.world}} lo={{lo}} hi={{hi}} max={{mx:.3f}} total={{tot:.0f}}", flush=True)
+nodes = ",".join(str(int(x)) for x in g.gather(3 - g.rank))  # e.g. each rank's NUMA node (bench.py)
+print(f"rank={{g.rank}} world={{g.world}} lo={{lo}} hi={{hi}} max={{mx:.3f}} total={{tot:.0f}} nodes={{nodes}}", flush=True)
 g.close()
 """
 
@@ -93,8 +94,8 @@ def test_gloo_world2_reduction(tmp_path):
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-2000:]
     lines = sorted(l for o, _ in outs for l in o.splitlines() if l.startswith("rank="))
-    assert lines[0] == "rank=0 world=2 lo=0 hi=2048 max=0.020 total=4096"
-    assert lines[1] == "rank=1 world=2 lo=2048 hi=4096 max=0.020 total=4096"
+    assert lines[0] == "rank=0 world=2 lo=0 hi=2048 max=0.020 total=4096 nodes=3,2"
+    assert lines[1] == "rank=1 world=2 lo=2048 hi=4096 max=0.020 total=4096 nodes=3,2"
 
 
 def _bench(args, env_extra=None, timeout=240):

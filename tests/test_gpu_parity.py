@@ -528,7 +528,19 @@ def test_encode_decode_object(gpu_ctx, n, k, M, length):
     gpu_ctx.decode_object(n, k, failed, cb.ptr, length, M, out.ptr, tail.ptr)
     gpu_ctx.sync()
     assert np.array_equal(out.download(), obj)
-    for b in (ob, par, tail, md5, cb, out):
+    # the strided form on the library's recover-heavy layout (StripeBatch::decodeFile's staging)
+    cst, sst = nxec.batch_layout(n, M, nxec.LAYOUT_RECOVER_HEAVY)
+    sst = max(sst, n * cst + 16)  # and a stripe stride with slack, so the strides really are used
+    padded = np.full((ns, sst), 0xA5, dtype=np.uint8)
+    for s in range(ns):
+        for c in range(n):
+            padded[s, c * cst: c * cst + M] = chunks[s, c]
+    pb = up(padded)
+    out.memset(0)
+    gpu_ctx.decode_object_ex(n, k, failed, pb.ptr, cst, sst, length, M, out.ptr, tail.ptr)
+    gpu_ctx.sync()
+    assert np.array_equal(out.download(), obj)
+    for b in (ob, par, tail, md5, cb, out, pb):
         b.free()
 
 
@@ -1251,4 +1263,62 @@ def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, 
     if ns > nf and p > 0:
         last = first + ns - 1
         assert m1[last, k].tobytes().hex() == hashlib.md5(p1[last, 0, :cl].tobytes()).hexdigest()
+    arena.free()
+
+
+@pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 6000), (16, 12, 2048, 9000), (6, 4, 1024, 5000)])
+def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
+    """More requests than the chip has slots (256 CUs x 16): the planner packs
+    several requests into a slot (longest first into the least loaded one) and
+    each lane's cursor walks them back to back.  Parity, tail arena and every
+    digest equal the separate launches (NXEC_FUSED_MD5=0) and the
+    one-request-per-slot form (NXEC_FILES_PACK=0, a second workgroup wave);
+    every digest of a sample of stripes equals hashlib's."""
+    import hashlib
+    p = n - k
+    rng = np.random.default_rng(nfiles + n)
+    lengths = [int(x) for x in rng.integers(1, 2 * k * M + 1, size=nfiles)]
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    offs, pos = [], 0
+    for L in lengths:
+        offs.append(pos)
+        pos += (L + 15) // 16 * 16
+    host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
+    arena = up(host)
+    out = {}
+    for fused, pack in (("1", "1"), ("1", "0"), ("0", "1")):
+        monkeypatch.setenv("NXEC_FUSED_MD5", fused)
+        monkeypatch.setenv("NXEC_FILES_PACK", pack)
+        par = nxec.DeviceBuffer(total * p * M)
+        par.memset(0)
+        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+        md5 = nxec.DeviceBuffer(total * n * 16)
+        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
+        out[fused + pack] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
+        for b in (par, tail, md5):
+            b.free()
+    p1, t1, m1 = out["11"]
+    for key in ("10", "01"):
+        pk, tk, mk = out[key]
+        assert np.array_equal(t1, tk), key
+        assert np.array_equal(m1, mk), key
+    g = 0
+    toff = 0
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        for s in range(ns):
+            cs = M if s < nf else cl
+            for key in ("10", "01"):
+                assert np.array_equal(p1[g + s, :, :cs], out[key][0][g + s, :, :cs]), (key, i, s)
+            if i % 97 == 0:  # hashlib on a sample: data chunks from the object / tail arena, parity
+                cls = (cl + 15) // 16 * 16
+                for c in range(k):
+                    src = host[o + (s * k + c) * M: o + (s * k + c) * M + M] if s < nf else \
+                        t1[toff + c * cls: toff + c * cls + cl]
+                    assert m1[g + s, c].tobytes() == hashlib.md5(src.tobytes()).digest(), (i, s, c)
+                for r in range(p):
+                    assert m1[g + s, k + r].tobytes() == hashlib.md5(p1[g + s, r, :cs].tobytes()).digest()
+        if ns > nf:
+            toff += k * ((cl + 15) // 16 * 16)
+        g += ns
     arena.free()

@@ -7,8 +7,16 @@
 // encode (k+p)*cs, 4-erasure decode (k+e)*cs.  A third leg calls
 // CodingUtils::encode (coding_util.hh:12-31, the agent's entry) on
 // preallocated buffers: the transport alone, without RSCode::encode's own
-// per-call chunk allocation + data copy (rs.cc:72-80).
+// per-call chunk allocation + data copy (rs.cc:72-80).  A fourth leg,
+// "writeFileStripe", is the whole coding side of the proxy's write of one
+// stripe with the reference's own Chunk handling: ChunkManager::encodeFile
+// (RSCode::encode, then file.chunks[i].move(stripe[i]), chunk_manager.cc:
+// 427-447), Chunk::computeMD5 of every chunk and the shallow event copies
+// (:172-179), the events and the file torn down; GiB/s of user data (k*cs per
+// stripe), the unit of bench.py cpu_baseline.write_path_with_md5.  Run it with
+// NXEC_CHUNK_MD5=0 for the host-hashed (OpenSSL) form.
 //
+// usage: dropin_rate [cs] [seconds] [all|agent|write] [threads,...]
 // Build: make tools   (build/dropin_rate)
 #include <atomic>
 #include <chrono>
@@ -36,11 +44,22 @@ int main(int argc, char **argv) {
   CodingOptions opt(n, k, false);
   Coding *code = CodingGenerator::genCoding(CodingScheme::RS, opt);
   if (!code) return 1;
-  // argv[3] = "agent": only the agent-service leg
+  // argv[3] = "agent": only the agent-service leg; "write": only the writeFileStripe leg
   const bool agent_only = argc > 3 && std::strcmp(argv[3], "agent") == 0;
-  for (int threads : {1, 4, 16}) {
+  const bool write_only = argc > 3 && std::strcmp(argv[3], "write") == 0;
+  std::vector<int> tlist0{1, 4, 16};
+  if (argc > 4) {
+    tlist0.clear();
+    for (const char *p = argv[4]; *p;) {
+      tlist0.push_back(std::atoi(p));
+      while (*p && *p != ',') p++;
+      if (*p == ',') p++;
+    }
+  }
+  for (int threads : tlist0) {
     if (agent_only) break;
-    for (int op = 0; op < 3; op++) {  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode
+    for (int op = write_only ? 3 : 0; op < 4; op++) {  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode,
+                                                       // 3 writeFileStripe (encode + MD5 of every chunk + events)
       std::atomic<long> stripes{0};
       std::atomic<bool> ok{true};
       const auto t0 = std::chrono::steady_clock::now();
@@ -66,6 +85,29 @@ int main(int argc, char **argv) {
             if (op == 0) {
               std::vector<Chunk> s2;
               if (!code->encode(data.data(), static_cast<length_t>(data.size()), s2, nullptr)) ok = false;
+            } else if (op == 3) {
+              // ChunkManager::encodeFile (chunk_manager.cc:427-447)
+              std::vector<Chunk> s2;
+              if (!code->encode(data.data(), static_cast<length_t>(data.size()), s2, nullptr)) ok = false;
+              Chunk *fileChunks = new Chunk[s2.size()];
+              for (size_t i = 0; i < s2.size(); i++) {
+                fileChunks[i].move(s2.at(i));
+                fileChunks[i].setChunkId(static_cast<int>(i));
+              }
+              // writeFileStripe (:149-179): MD5 of each chunk, then a borrowed view per event
+              Chunk *events = new Chunk[s2.size()];
+              for (size_t i = 0; i < s2.size(); i++) {
+                if (!fileChunks[i].computeMD5()) ok = false;
+                events[i] = fileChunks[i];
+                events[i].freeData = false;
+              }
+              if (first) {  // verify the first stripe's digests (not the path)
+                for (size_t i = 0; i < s2.size(); i++)
+                  if (!events[i].verifyMD5()) ok = false;
+                first = false;
+              }
+              delete[] events;
+              delete[] fileChunks;
             } else if (op == 2) {
               if (!CodingUtils::encode(data.data(), k, par.data(), n - k, cs, m.data())) ok = false;
             } else {
@@ -81,14 +123,19 @@ int main(int argc, char **argv) {
         });
       for (auto &th : pool) th.join();
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      const double bytes = static_cast<double>(stripes) * (k + (op != 1 ? n - k : e)) * cs;
-      static const char *names[3] = {"RSCode::encode", "RSCode::decode", "CodingUtils::encode"};
+      const double bytes = static_cast<double>(stripes) * (op == 3 ? k : k + (op != 1 ? n - k : e)) * cs;
+      static const char *names[4] = {"RSCode::encode", "RSCode::decode", "CodingUtils::encode", "writeFileStripe"};
       std::printf("{\"path\": \"%s per stripe\", \"threads\": %d, \"chunk\": %d, \"stripes\": %ld, "
-                  "\"GiB_s\": %.2f, \"ms_per_call\": %.3f, \"ok\": %s}\n",
-                  names[op], threads, cs, static_cast<long>(stripes), bytes / dt / (1 << 30),
-                  1e3 * dt * threads / static_cast<double>(stripes), ok ? "true" : "false");
+                  "\"GiB_s%s\": %.2f, \"ms_per_call\": %.3f, \"chunk_md5\": %d, \"ok\": %s}\n",
+                  names[op], threads, cs, static_cast<long>(stripes), op == 3 ? "_user_data" : "",
+                  bytes / dt / (1 << 30), 1e3 * dt * threads / static_cast<double>(stripes), nxec_chunk_md5_mode(),
+                  ok ? "true" : "false");
       std::fflush(stdout);
     }
+  }
+  if (write_only) {
+    delete code;
+    return 0;
   }
   // agent service: nxec_agent_encode_batch calls of 64
   // ENC_CHUNK_REQ partial encodes each (4 local chunks x 1 coefficient row ->
