@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
     auto load = [&](int step, u32x4(&d)[K]) {
 #pragma unroll
-      for (int j = 0; j < K; j++) d[j] = dev::ld_stream(sp[j] + step * sstep);
+      for (int j = 0; j < K; j++) d[j] = dev::ld_global_stream(sp[j] + step * sstep);
     };
     auto run = [&](int step, const u32x4(&d)[K]) {
       uint8_t *rb = row + (step & 1) * buf_bytes;
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          dev::st_stream(dp[r] + step * sstep, pv);
+          dev::st_global_stream(dp[r] + step * sstep, pv);
           if (act) *reinterpret_cast<u32x4 *>(rb + (hsrc + r) * kEmRow) = pv;
         }
       }
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 #pragma unroll
       for (int j = 0; j < K; j++) {
         if (nb == 16) {
-          d[j] = dev::ld_stream(sp[j] + off);
+          d[j] = dev::ld_global_stream(sp[j] + off);
         } else {
           uint32_t w[4] = {0, 0, 0, 0};
           for (int i = 0; i < nb; i++) w[i / 4] |= static_cast<uint32_t>(sp[j][off + i]) << (8 * (i % 4));
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
         if (r < a.p) {
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
           if (nb == 16) {
-            dev::st_stream(dp[r] + off, pv);
+            dev::st_global_stream(dp[r] + off, pv);
           } else {
             const uint32_t w[4] = {pv.x, pv.y, pv.z, pv.w};
             for (int i = 0; i < nb; i++) dp[r][off + i] = static_cast<uint8_t>(w[i / 4] >> (8 * (i % 4)));
@@ -653,9 +653,9 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         // shares its boundary lines between consecutive steps; streaming
         // loads fetched them once per step
         if (a.cached_loads)
-          d[j] = *reinterpret_cast<const u32x4 *>(sp[j] + off);
+          d[j] = dev::ld_global(sp[j] + off);
         else
-          d[j] = dev::ld_stream(sp[j] + off);
+          d[j] = dev::ld_global_stream(sp[j] + off);
       }
       if (++lt == lT) {
         if (lr + 1 < cnt) {  // next request of the slot (pointers from the LDS table)
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          dev::st_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
+          dev::st_global_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
           if (ok) *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = pv;
         }
       }

@@ -5,7 +5,9 @@ profiles/.  Usage:
   pmc_label.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR SOURCE_CMD LABEL:BYTES [LABEL:BYTES ...]
 LABEL:BYTES pairs are matched to the dispatches in order (repeat the list per
 step as the bench issues it)."""
+import hashlib
 import json
+import os
 import subprocess
 import sys
 
@@ -21,8 +23,12 @@ for r, (lab, alg) in zip(rows, labels):
     r.update(op=lab, algorithmic_bytes=alg, traffic_over_algorithmic=round(r["hbm_bytes"] / alg, 5),
              frac_of_8TBs_fetch_pass=round(alg / (r["ms_fetch_pass"] * 1e-3) / 8e12, 4))
     disp.append(r)
+# the library the passes measured (labelled right after the run, before any rebuild; LIB_SHA16 overrides)
+lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nexoedge_amd", "lib", "libnxec.so")
+lib_sha16 = os.environ.get("LIB_SHA16") or hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]
 print(json.dumps({
     "source": f"rocprofv3 --pmc FETCH_SIZE --kernel-trace and --pmc WRITE_SIZE --kernel-trace, separate passes of: {cmd}",
+    "lib_sha16": lib_sha16,
     "gfx950_correction": "read_bytes = 2 * FETCH_SIZE * 1024 (FETCH_SIZE counts half the bytes of 16-B/lane streaming "
                          "reads, MI355X_MICROARCH.md HBM); write_bytes = WRITE_SIZE * 1024",
     "note": "ms_fetch_pass is the kernel-trace duration inside the counter pass (profiled clocks run 2-5% lower)",
