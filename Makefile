@@ -12,7 +12,7 @@ CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip \
-            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_numa.cpp $(CSRC)/nxec_config.cpp \
+            $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_digest_place.cpp $(CSRC)/nxec_numa.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_device.h $(wildcard $(CSRC)/coding/*.hh)
@@ -56,7 +56,7 @@ $(OBJDIR)/%.o: $(CSRC)/% $(HDRS)
 
 $(LIBDIR)/libnxec.so: $(LIB_OBJS)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(LIB_OBJS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(LIB_OBJS) -lcrypto -o $@
 
 oracle/liboracle.so: oracle/nxec_oracle.c oracle/nxec_cpu_simd.c oracle/nxec_oracle.h
 	gcc -O2 -std=c11 -Wall -fPIC -shared oracle/nxec_oracle.c oracle/nxec_cpu_simd.c -o $@ -lpthread
@@ -98,7 +98,7 @@ build/san/$(1)/obj/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p $$(dir $$@)
 	$(HIPCC) $(SAN_CFLAGS) $(2) -c $$< -o $$@
 build/san/$(1)/libnxec.so: $(patsubst $(CSRC)/%,build/san/$(1)/obj/%.o,$(SAN_SRCS))
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(2) $$^ -o $$@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(2) $$^ -lcrypto -o $$@
 build/san/$(1)/host_sanity_test: tests/cpp/host_sanity_test.cc build/san/$(1)/libnxec.so $(HDRS)
 	$(HIPCC) -O1 -g $(CXXSTD) $(2) -Iinclude -I$(CSRC) $$< -Lbuild/san/$(1) -lnxec \
 	    -Wl,-rpath,'$$$$ORIGIN' -lcrypto -lpthread -o $$@

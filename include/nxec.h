@@ -96,6 +96,21 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
  * Synchronous; thread-safe. */
 int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
                          unsigned char *const *coding, unsigned char *md5_data, unsigned char *md5_code);
+/* Where nxec_encode_host_md5 hashes (the coding always runs on the GPU):
+ * NXEC_DIGEST_GPU -- in the coding kernel (one ~10 ms/MiB MD5 chain per chunk,
+ * thousands at once); NXEC_DIGEST_HOST -- OpenSSL on the library's digest
+ * pool (NXEC_DIGEST_THREADS, default min(16, CPUs)) plus the calling thread,
+ * the inputs' digests overlapping the GPU pass; NXEC_DIGEST_AUTO (default) --
+ * per call, whichever the measured pool backlog and GPU latency say finishes
+ * first (few callers: the pool; many: the surplus on the GPU).  Environment:
+ * NXEC_DIGEST_PLACE=auto|gpu|host.  Returns the previous mode, or < 0. */
+#define NXEC_DIGEST_AUTO 0
+#define NXEC_DIGEST_GPU 1
+#define NXEC_DIGEST_HOST 2
+int nxec_set_digest_placement(int mode);
+int nxec_digest_placement(void);
+/* calls placed on the host pool / the GPU so far, and the pool's threads */
+int nxec_digest_place_stats(unsigned long long *host_calls, unsigned long long *gpu_calls, int *host_threads);
 
 /* ---------------------------------------------------------------------------
  * 2b. The boundary under the names of SURVEY §8b (thin forms of the above,

@@ -14,6 +14,20 @@ namespace nxec {
 // copies of the host entry points); returns when all are done.
 void host_parallel_for(int n, const std::function<void(int)> &fn);
 
+// Digest placement of nxec_encode_host_md5 (nxec_digest_place.cpp): true if
+// the call's nhash digests of len bytes go to the host pool (their bytes are
+// then reserved in its backlog), false for the GPU coding pass.
+bool digest_place_host(int64_t len, int nhash);
+// a GPU-placed call took `ms` end to end (feeds the placement's estimate)
+void digest_gpu_observe(int64_t len, double ms);
+// every call, on its way out (the placement's model of the callers' cycle)
+double digest_clock_ns();
+void digest_call_done(double start_ns);
+// the host-placed call: GPU coding, digests on the pool and the calling thread
+int encode_host_md5_host_digests(int len, int k, int rows, const unsigned char *coeffs,
+                                 const unsigned char *const *data, unsigned char *const *coding,
+                                 unsigned char *md5_data, unsigned char *md5_code);
+
 // Sets the calling thread's last-error message and returns `code`.
 int set_error(int code, const char *fmt, ...);
 bool valid_nk(int n, int k);

@@ -2523,8 +2523,25 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
     for (int r = 0; md5_code && r < rows; r++) std::memcpy(md5_code + 16 * r, empty, 16);
     return NXEC_OK;
   }
+  // digests on the host pool or in the coding kernel (nxec_digest_place.cpp)
+  const double t_call = digest_clock_ns();
+  if (digest_place_host(len, (md5_data ? k : 0) + (md5_code ? rows : 0))) {
+    const int hrc = encode_host_md5_host_digests(len, k, rows, coeffs, data, coding, md5_data, md5_code);
+    digest_call_done(t_call);
+    return hrc;
+  }
+  int rc = NXEC_OK;
+  struct Observe {  // the GPU-placed call's latency, whichever way it returns
+    int64_t len;
+    const int &rc;
+    double t0;
+    ~Observe() {
+      if (rc == NXEC_OK) digest_gpu_observe(len, (digest_clock_ns() - t0) * 1e-6);
+      digest_call_done(t0);
+    }
+  } observe{len, rc, t_call};
   nxec_ctx_t *ctx = nullptr;
-  int rc = default_ctx(&ctx);
+  rc = default_ctx(&ctx);
   if (rc) return rc;
   if ((rc = ensure_device(ctx->device))) return rc;
   DigestJob job;
@@ -2558,7 +2575,8 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
     r.outputs = coding;
     r.md5 = md5_code;
     r.md5_inputs = md5_data;
-    return nxec_agent_encode_batch(ctx, &r, 1, len, 0);
+    rc = nxec_agent_encode_batch(ctx, &r, 1, len, 0);
+    return rc;
   }
   std::unique_lock<std::mutex> lk(ctx->dg_mu);
   ctx->dg_pending.push_back(&job);
@@ -2597,7 +2615,8 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
   }
   lk.unlock();
   if (job.rc != NXEC_OK) g_last_error = job.error;
-  return job.rc;
+  rc = job.rc;
+  return rc;
 }
 
 int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gftbls, const unsigned char *const *data,

@@ -258,6 +258,25 @@ static void ini_files() {
   for (const std::string &f : {sc, two, bad, dup, px}) unlink(f.c_str());
 }
 
+// the digest pool of nxec_encode_host_md5 (nxec_digest_place.cpp) from many
+// threads: placed on the host, each call queues its inputs' digests, then the
+// coding fails (no device here) and the call drains its own digests before it
+// returns the error -- the queue, the helping callers and the pool threads
+// under ASan / UBSan / TSan
+static void digest_pool(int t) {
+  const int cs = 70000 + t, k = 4;
+  std::vector<std::vector<unsigned char>> d(k, std::vector<unsigned char>(cs, static_cast<unsigned char>(t)));
+  std::vector<const unsigned char *> dp(k);
+  for (int j = 0; j < k; j++) dp[j] = d[j].data();
+  std::vector<unsigned char> out(cs), md_in(16 * k), md_out(16);
+  unsigned char *op = out.data();
+  const unsigned char coef[4] = {1, 1, 1, 1};
+  for (int it = 0; it < 20; it++) {
+    const int rc = nxec_encode_host_md5(cs, k, 1, coef, dp.data(), &op, md_in.data(), md_out.data());
+    CHECK(rc == NXEC_OK || rc == NXEC_ERR_NODEV || rc == NXEC_ERR_HIP, "host-placed call returns");
+  }
+}
+
 int main() {
   gf_and_planning();
   argument_validation();
@@ -265,6 +284,11 @@ int main() {
   std::vector<std::thread> th;
   for (int t = 0; t < 8; t++) th.emplace_back(surface, t);
   for (auto &t : th) t.join();
+  const int prev = nxec_set_digest_placement(NXEC_DIGEST_HOST);
+  std::vector<std::thread> dt;
+  for (int t = 0; t < 12; t++) dt.emplace_back(digest_pool, t);
+  for (auto &t : dt) t.join();
+  nxec_set_digest_placement(prev);
   std::printf("%s %d failures\n", g_fail ? "FAILED" : "PASSED", g_fail.load());
   return g_fail ? 1 : 0;
 }

@@ -193,3 +193,56 @@ def test_arena_bound_defaults_to_a_fraction_of_ram():
     ram = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGESIZE")
     assert _lib.lib.nxec_host_arena_cap() == min(16 << 30, ram // 8)
     assert _lib.lib.nxec_host_arena_trim(0) == 0
+
+
+PLACE_ENV = r"""
+import ctypes, sys
+sys.path.insert(0, {root!r})
+from nexoedge_amd import _lib
+print("MODE", _lib.lib.nxec_digest_placement(), flush=True)
+"""
+
+
+def test_digest_placement_modes():
+    """include/nxec.h §2: nxec_encode_host_md5's digest placement -- auto by
+    default, NXEC_DIGEST_PLACE=gpu|host pins it, the setter returns the
+    previous mode and rejects unknown ones."""
+    lib = _lib.lib
+    prev = lib.nxec_digest_placement()
+    try:
+        assert lib.nxec_set_digest_placement(1) == prev
+        assert lib.nxec_digest_placement() == 1
+        assert lib.nxec_set_digest_placement(2) == 1
+        assert lib.nxec_set_digest_placement(7) == _lib.NXEC_ERR_INVALID
+        assert lib.nxec_digest_placement() == 2
+    finally:
+        lib.nxec_set_digest_placement(prev)
+    h, g, t = ctypes.c_ulonglong(), ctypes.c_ulonglong(), ctypes.c_int()
+    assert lib.nxec_digest_place_stats(ctypes.byref(h), ctypes.byref(g), ctypes.byref(t)) == 0
+    assert 0 <= t.value <= 16
+    for env, want in ((None, 0), ("auto", 0), ("gpu", 1), ("host", 2)):
+        e = dict(os.environ)
+        e.pop("NXEC_DIGEST_PLACE", None)
+        if env:
+            e["NXEC_DIGEST_PLACE"] = env
+        out = subprocess.run(["python", "-c", PLACE_ENV.format(root=ROOT)], capture_output=True, text=True,
+                             env=e, timeout=120).stdout
+        assert f"MODE {want}" in out, (env, out)
+
+
+@pytest.mark.skipif(nxec.device_count() > 0, reason="a GPU is visible")
+def test_host_placed_digests_fail_loudly_without_a_device():
+    """A call placed on the host digest pool still codes on the GPU: with no
+    device it returns the error (no CPU coding) after its queued input digests
+    have drained -- no hang, the pool stays usable."""
+    import numpy as np
+
+    lib = _lib.lib
+    prev = lib.nxec_set_digest_placement(2)
+    try:
+        for _ in range(3):
+            with pytest.raises(nxec.NxecError) as e:
+                nxec.encode_host_md5(np.ones((1, 3), dtype=np.uint8), [np.arange(70000, dtype=np.uint8)] * 3)
+            assert e.value.code == _lib.NXEC_ERR_NODEV
+    finally:
+        lib.nxec_set_digest_placement(prev)

@@ -29,12 +29,33 @@ def md5(a):
     return np.frombuffer(hashlib.md5(np.ascontiguousarray(a).tobytes()).digest(), dtype=np.uint8)
 
 
+PLACES = {"auto": 0, "gpu": 1, "host": 2}
+
+
+@pytest.fixture
+def placement(request):
+    """nxec_encode_host_md5's digest placement for the test (include/nxec.h §2)."""
+    prev = lib.nxec_set_digest_placement(PLACES[request.param])
+    assert prev >= 0
+    yield request.param
+    lib.nxec_set_digest_placement(prev)
+
+
+def place_stats():
+    h, g, t = C.c_ulonglong(), C.c_ulonglong(), C.c_int()
+    lib.nxec_digest_place_stats(C.byref(h), C.byref(g), C.byref(t))
+    return h.value, g.value
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("placement", ["gpu", "host"], indirect=True)
 @pytest.mark.parametrize("n,k", [(14, 10), (6, 4), (4, 2), (16, 12), (20, 16), (5, 1)])
 @pytest.mark.parametrize("cs", [1 << 20, 65537, 4096, 1000, 31])
 @pytest.mark.parametrize("kind", ["arena", "pageable", "mixed"])
-def test_encode_host_md5_rs_stripe(gpu_ctx, n, k, cs, kind):
-    """RSCode::encode's call: parity + the digests of all n chunks."""
+def test_encode_host_md5_rs_stripe(gpu_ctx, placement, n, k, cs, kind):
+    """RSCode::encode's call: parity + the digests of all n chunks, hashed in
+    the coding kernel (gpu) or on the host digest pool (host)."""
+    h0, g0 = place_stats()
     rng = np.random.default_rng(n * 1000 + k + cs)
     arena = Arena()
     try:
@@ -50,12 +71,15 @@ def test_encode_host_md5_rs_stripe(gpu_ctx, n, k, cs, kind):
             assert np.array_equal(md_out[r], md5(outs[r])), f"parity digest {r}"
         for j in range(k):
             assert np.array_equal(md_in[j], md5(data[j])), f"data digest {j}"
+        h1, g1 = place_stats()
+        assert (h1 - h0, g1 - g0) == ((1, 0) if placement == "host" else (0, 1))
     finally:
         arena.free()
 
 
 @pytest.mark.gpu
-def test_encode_host_md5_outputs_only_and_empty(gpu_ctx):
+@pytest.mark.parametrize("placement", ["gpu", "host"], indirect=True)
+def test_encode_host_md5_outputs_only_and_empty(gpu_ctx, placement):
     """RSCode::decode(isRepair) / CodingUtils::encode: only the outputs hashed;
     a zero-length call gives the empty message's digest."""
     rng = np.random.default_rng(5)
@@ -73,11 +97,13 @@ def test_encode_host_md5_outputs_only_and_empty(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_encode_host_md5_concurrent_callers_share_rounds(gpu_ctx):
+@pytest.mark.parametrize("placement", ["gpu", "auto"], indirect=True)
+def test_encode_host_md5_concurrent_callers_share_rounds(gpu_ctx, placement):
     """16 threads each encoding RS(10,4) stripes with digests at once (the
     proxy's workers): every stripe's parity and 14 digests are right whatever
-    round it joined."""
+    round it joined -- or, under auto placement, wherever each call hashed."""
     n, k, cs = 14, 10, 256 << 10
+    h0, g0 = place_stats()
     enc = nxec.gen_rs_matrix(n, k)[k:]
     errors = []
 
@@ -108,6 +134,11 @@ def test_encode_host_md5_concurrent_callers_share_rounds(gpu_ctx):
     for x in th:
         x.join()
     assert not errors, errors[:10]
+    h1, g1 = place_stats()
+    assert (h1 - h0) + (g1 - g0) == 64
+    if placement == "gpu":
+        assert h1 == h0
+    print(f"placement {placement}: host calls {h1 - h0}, gpu calls {g1 - g0}")
 
 
 def _run(code, env_extra, timeout=300):

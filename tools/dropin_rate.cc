@@ -62,6 +62,9 @@ int main(int argc, char **argv) {
                                                        // 3 writeFileStripe (encode + MD5 of every chunk + events)
       std::atomic<long> stripes{0};
       std::atomic<bool> ok{true};
+      unsigned long long h0 = 0, g0 = 0, h1 = 0, g1 = 0;
+      int dthreads = 0;
+      nxec_digest_place_stats(&h0, &g0, &dthreads);
       const auto t0 = std::chrono::steady_clock::now();
       std::vector<std::thread> pool;
       for (int t = 0; t < threads; t++)
@@ -123,13 +126,16 @@ int main(int argc, char **argv) {
         });
       for (auto &th : pool) th.join();
       const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      nxec_digest_place_stats(&h1, &g1, &dthreads);
       const double bytes = static_cast<double>(stripes) * (op == 3 ? k : k + (op != 1 ? n - k : e)) * cs;
       static const char *names[4] = {"RSCode::encode", "RSCode::decode", "CodingUtils::encode", "writeFileStripe"};
+      static const char *place_names[4] = {"auto", "gpu", "host", "?"};
       std::printf("{\"path\": \"%s per stripe\", \"threads\": %d, \"chunk\": %d, \"stripes\": %ld, "
-                  "\"GiB_s%s\": %.2f, \"ms_per_call\": %.3f, \"chunk_md5\": %d, \"ok\": %s}\n",
+                  "\"GiB_s%s\": %.2f, \"ms_per_call\": %.3f, \"chunk_md5\": %d, \"digest_place\": \"%s\", "
+                  "\"digest_calls_host\": %llu, \"digest_calls_gpu\": %llu, \"digest_threads\": %d, \"ok\": %s}\n",
                   names[op], threads, cs, static_cast<long>(stripes), op == 3 ? "_user_data" : "",
                   bytes / dt / (1 << 30), 1e3 * dt * threads / static_cast<double>(stripes), nxec_chunk_md5_mode(),
-                  ok ? "true" : "false");
+                  place_names[nxec_digest_placement() & 3], h1 - h0, g1 - g0, dthreads, ok ? "true" : "false");
       std::fflush(stdout);
     }
   }
