@@ -206,8 +206,8 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    ("rs10_4", 1 << 20, "auto"): ("r02_pmc_rs10_4.json", ("encode", "recover")),
-    ("rs10_4", 1 << 20, "natural"): ("r02_pmc_rs10_4.json", ("encode", "recover")),
+    ("rs10_4", 1 << 20, "auto"): ("r03_pmc_rs10_4.json", ("encode", "recover")),
+    ("rs10_4", 1 << 20, "natural"): ("r03_pmc_rs10_4.json", ("encode", "recover")),
     ("rs10_4", 1 << 20, "recover"): ("r02_pmc_rs10_4_layout_recover.json", ("encode", "recover")),
     ("mixed16", 4 << 20, "auto"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
     ("mixed16", 4 << 20, "recover"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
