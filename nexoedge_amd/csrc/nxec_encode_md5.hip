@@ -394,6 +394,13 @@ template <int K>
 constexpr int gm_depth() {
   return (200 - 2 * K) / (4 * K) >= 8 ? 8 : (200 - 2 * K) / (4 * K) < 2 ? 2 : (200 - 2 * K) / (4 * K);
 }
+// k_files_md5 reads HBM (a step of ~2 us is many load latencies), and its
+// last-stripe path needs registers of its own: at most 3 steps in flight,
+// 2 from k = 13 (no spills through k = 16)
+template <int K>
+constexpr int fm_depth() {
+  return K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
+}
 
 // The agent's requests (container_manager.cc:221-258 partial encodes and
 // agent.cc:240-415 repairs, then the MD5 of every output, agent.cc:342): the
@@ -586,7 +593,8 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   const int nh = K + a.p;
   const int S = a.slots_per_group;
   const int L = a.max_list;
-  const int rec = K + a.p + 2;  // request record: K sources, p outputs, digest base, length
+  // request record: K sources, p outputs, digest base, length, tail source, tail bytes
+  const int rec = K + a.p + 4;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
   const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
@@ -606,8 +614,12 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         v = reinterpret_cast<uint64_t>(a.dst_ptrs[r * a.p + (f - K)]);
       else if (f == K + a.p)
         v = reinterpret_cast<uint64_t>(a.dig_ptrs[r]);
-      else
+      else if (f == K + a.p + 1)
         v = static_cast<uint64_t>(a.lens[r]);
+      else if (f == K + a.p + 2)
+        v = a.tail_src ? reinterpret_cast<uint64_t>(a.tail_src[r]) : 0;
+      else
+        v = a.tail_rem ? static_cast<uint64_t>(a.tail_rem[r]) : 0;
     }
     rq[i] = v;
   }
@@ -638,24 +650,62 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     const uint8_t *sp[K];
     // a lane whose column holds no byte of the request (chunks under 256
     // bytes) reads the scratch line: nothing past a chunk's 16-byte padding is read
+    // A last stripe read from its object (tail source != 0): data chunk j is
+    // tail bytes [j*cl, (j+1)*cl), valid below min((j+1)*cl, rem): `tl` = cl
+    // (0 for a full stripe), `jf` = chunks wholly valid, `last` = the valid
+    // bytes of chunk jf (32-bit: cl <= 1 GiB), `end` = the end of the tail's
+    // last 16-byte line (nothing at or past it is read)
+    auto tail_state = [&](int li, int64_t cl, uint32_t &tl, uint32_t &jf, uint32_t &last, const uint8_t *&end) {
+      const uint64_t tb = act ? q[li * rec + K + a.p + 2] : uint64_t(0);
+      const int64_t rem = act ? static_cast<int64_t>(q[li * rec + K + a.p + 3]) : int64_t(0);
+      const int64_t f = tb && cl > 0 ? min(rem / cl, static_cast<int64_t>(K)) : 0;
+      tl = tb ? static_cast<uint32_t>(cl) : 0u;
+      jf = static_cast<uint32_t>(f);
+      last = f < K && tb ? static_cast<uint32_t>(rem - f * cl) : 0u;
+      end = reinterpret_cast<const uint8_t *>((tb + static_cast<uint64_t>(rem) + 15) & ~uint64_t(15));
+    };
+    auto valid_of = [](int j, uint32_t tl, uint32_t jf, uint32_t last) {
+      return static_cast<int32_t>(static_cast<uint32_t>(j) < jf ? tl : static_cast<uint32_t>(j) == jf ? last : 0u);
+    };
+    // source pointers of the lane's column: a full stripe's chunks, a tail's
+    // object bytes (at any byte), or -- a lane whose column holds no byte of
+    // the request (chunks under 256 bytes) -- the scratch line: nothing past a
+    // chunk's 16-byte padding is read
     auto set_src = [&](int li, bool has) {
+      const uint64_t tb = act ? q[li * rec + K + a.p + 2] : uint64_t(0);
+      const int64_t cl = len_of(li);
 #pragma unroll
       for (int j = 0; j < K; j++)
-        sp[j] = act && has ? reinterpret_cast<const uint8_t *>(q[li * rec + j]) + v * 16 : a.scratch + v * 16;
+        sp[j] = act && has ? (tb ? reinterpret_cast<const uint8_t *>(tb) + j * cl
+                                 : reinterpret_cast<const uint8_t *>(q[li * rec + j])) + v * 16
+                           : a.scratch + v * 16;
     };
     set_src(0, tmax_of(len0) >= 0);
+    uint32_t ltl, ljf, llast;
+    const uint8_t *lend;
+    tail_state(0, len0, ltl, ljf, llast, lend);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
 #pragma unroll
       for (int j = 0; j < K; j++) {
-        // plain (cached) loads: a chunk that is not 128-byte aligned (a tail
-        // arena chunk at a 16-byte stride, an object at any 16-byte offset)
-        // shares its boundary lines between consecutive steps; streaming
-        // loads fetched them once per step
+        // a tail chunk's 16 bytes are read where they lie (global loads take
+        // any byte address), except where they would run past the tail's
+        // last 16-byte line: that lane reads the aligned line holding its
+        // first byte (the compute step shifts it into place), or the scratch
+        // line once nothing of the tail is left
+        const uint8_t *pj = sp[j] + off;
+        if (ltl)
+          pj = pj + 16 <= lend ? pj
+               : pj < lend     ? reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pj) & ~uintptr_t(15))
+                               : a.scratch + v * 16;
+        // plain (cached) loads: a chunk that is not 128-byte aligned (an
+        // object at any 16-byte offset, a tail at any byte) shares its
+        // boundary lines between consecutive steps; streaming loads fetched
+        // them once per step
         if (a.cached_loads)
-          d[j] = dev::ld_global(sp[j] + off);
+          d[j] = dev::ld_global(pj);
         else
-          d[j] = dev::ld_global_stream(sp[j] + off);
+          d[j] = dev::ld_global_stream(pj);
       }
       if (++lt == lT) {
         if (lr + 1 < cnt) {  // next request of the slot (pointers from the LDS table)
@@ -665,6 +715,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           lT = steps_of(ln);
           ltcl = max(tmax_of(ln), 0);
           set_src(lr, tmax_of(ln) >= 0);
+          tail_state(lr, ln, ltl, ljf, llast, lend);
         } else {
           lt = lT - 1;  // past the slot's end: re-read the last step
         }
@@ -673,6 +724,12 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // compute cursor
     int cr = 0, ct = 0, cT = lT, ctmax = act ? tmax_of(len0) : -1;
     bool live = act;
+    uint32_t ctl = ltl, cjf = ljf, clast = llast;
+    const uint8_t *cend = lend;
+    // the tail source and the tail arena's chunk 0 (chunk j at + j*cls), kept
+    // in registers: no per-step read of the request table
+    const uint8_t *ctb = act ? reinterpret_cast<const uint8_t *>(q[K + a.p + 2]) : nullptr;
+    uint8_t *ctd = act ? reinterpret_cast<uint8_t *>(q[0]) : nullptr;
     uint8_t *dp[kMaxRowsPerPass];
     auto set_dst = [&](int li) {
 #pragma unroll
@@ -680,20 +737,62 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         dp[r] = act && r < a.p ? reinterpret_cast<uint8_t *>(q[li * rec + K + r]) + v * 16 : a.scratch;
     };
     set_dst(0);
+    // a tail chunk's 16 bytes at column v of step ct, at the chunk's valid end
+    // (the lane's bytes run past it): a lane whose load was the aligned line
+    // holding its first byte shifts that line into place, then every byte
+    // from the valid end on is zeroed (the reference's zero padding)
+    auto tail_end = [&](int j, u32x4 x, int32_t nv) {
+      const int32_t pos = ct * kEncMd5Step + v * 16;
+      const uint8_t *addr = ctb + static_cast<int64_t>(j) * ctl + pos;
+      if (addr + 16 > cend) {
+        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(addr)) & 15u, qd = sh >> 2, rb = sh & 3u;
+        const uint32_t w[8] = {x.x, x.y, x.z, x.w, 0u, 0u, 0u, 0u};
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const uint32_t lo = (qd & 2u) ? ((qd & 1u) ? w[i + 3] : w[i + 2]) : ((qd & 1u) ? w[i + 1] : w[i]);
+          const uint32_t up = (qd & 2u) ? ((qd & 1u) ? w[i + 4] : w[i + 3]) : ((qd & 1u) ? w[i + 2] : w[i + 1]);
+          o[i] = __builtin_amdgcn_alignbyte(up, lo, rb);
+        }
+        x = u32x4{o[0], o[1], o[2], o[3]};
+      }
+      const int32_t n = max(nv, 0);
+      uint32_t m[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int keep = n - 4 * i;
+        m[i] = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+      }
+      return u32x4{x.x & m[0], x.y & m[1], x.z & m[2], x.w & m[3]};
+    };
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
+      const bool tl = live && ctl != 0;
       uint8_t *rb = row + (step & 1) * buf_bytes;
+      const int32_t pos = ct * kEncMd5Step + v * 16;
+      const int64_t cls = (static_cast<int64_t>(ctl) + 15) / 16 * 16;
       uint32_t acc[16];
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = 0;
 #pragma unroll
       for (int j = 0; j < K; j += 2) {
-        if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
-          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = d[j];
-          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = d[j + 1];
+        const int j1 = j + 1 < K ? j + 1 : j;
+        u32x4 x0 = d[j], x1 = d[j1];
+        if (tl) {
+          const int32_t nv0 = valid_of(j, ctl, cjf, clast) - pos, nv1 = valid_of(j1, ctl, cjf, clast) - pos;
+          if (nv0 < 16) x0 = tail_end(j, x0, nv0);
+          if (nv1 < 16) x1 = tail_end(j1, x1, nv1);
+          if (ok) {  // the zero-padded data chunks into the tail arena
+            dev::st_global_stream(ctd + j * cls + pos, x0);
+            if (j + 1 < K) dev::st_global_stream(ctd + j1 * cls + pos, x1);
+          }
         }
-        lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+        if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
+          *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = x0;
+          if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = x1;
+        }
+        lookup_pair(j, j + 1 < K, x0, x1, acc);
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
       }
@@ -717,12 +816,15 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           cT = steps_of(ln);
           ctmax = tmax_of(ln);
           set_dst(cr);
+          tail_state(cr, ln, ctl, cjf, clast, cend);
+          ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
+          ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
         } else {
           live = false;
         }
       }
     };
-    constexpr int D = gm_depth<K>();
+    constexpr int D = fm_depth<K>();
     u32x4 ring[D][K];
 #pragma unroll
     for (int j = 0; j < D - 1; j++) load(ring[j]);
@@ -975,7 +1077,7 @@ void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cu
   }
   S = std::max<int64_t>(S, 1);
   const int64_t lds_free = kEmLds - int64_t(k) * 1024 - 2 * S * nh * kEmRow;
-  const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 2) * 8));
+  const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 4) * 8));
   std::vector<std::vector<int32_t>> lists(static_cast<size_t>(G));
   std::vector<int64_t> load(static_cast<size_t>(G), 0);
   if (G == R) {
@@ -1045,7 +1147,7 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
     return set_error(NXEC_ERR_INVALID, "files+md5: %lld slots of %d chunks per workgroup", static_cast<long long>(S), nh);
   const int64_t grid = (a.nslots + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
-  const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 2) * 8;
+  const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
   hipLaunchKernelGGL(kFm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);

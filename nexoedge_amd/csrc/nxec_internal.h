@@ -232,9 +232,10 @@ int launch_gather_md5(const GatherMd5Args &a, int num_cus, void *stream);
 // k sources src_ptrs[s*k + j] into p outputs dst_ptrs[s*p + r] and hashes
 // all k + p chunks, lens[s] bytes each, digest of chunk c (sources first) at
 // dig_ptrs[s] + c*16.  Bytes up to the next multiple of 16 past lens[s] are
-// readable (and zero for a zero-padded last stripe); outputs are written up
-// to that multiple.  Every pointer 16-byte aligned (digests any); tables in
-// device memory.
+// readable; outputs are written up to that multiple.  A last stripe
+// (tail_src[s] set) reads its sources from the object instead and writes
+// them zero-padded to src_ptrs.  Every pointer 16-byte aligned (digests and
+// tail_src any); tables in device memory.
 //
 // Requests are packed into slots (one stripe's worth of code and hash lanes
 // of a workgroup): slot g runs requests slot_reqs[slot_first[g] ..
@@ -261,6 +262,14 @@ struct FilesMd5Args {
   int32_t max_list;           // longest slot list (LDS request table rows per slot)
   int32_t cached_loads;       // plain loads (default); NXEC_FILES_LOADS=0 streaming (A/B)
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
+  // A file's last stripe read straight from its object (no pad copy):
+  // tail_src[s] = the object's bytes past its full stripes (any alignment;
+  // nullptr for a full stripe), tail_rem[s] = how many.  Data chunk j of
+  // such a stripe is object bytes [j*lens[s], (j+1)*lens[s]) zero-padded;
+  // the kernel codes and hashes it and also writes it, so padded up to the
+  // next multiple of 16, to src_ptrs[s*k + j] (the tail arena).
+  const uint8_t *const *tail_src;
+  const int64_t *tail_rem;
 };
 // Slot plan for `lens` (descending): fills slot_first / slot_reqs / wg_steps
 // and the args' nslots / slots_per_group / max_list.  NXEC_FILES_PACK=0 gives

@@ -1004,14 +1004,19 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   // 16-byte aligned (else they join the byte-capable list kernel)
   const bool ragged_ok = p > 0 && M % 16 == 0 && (reinterpret_cast<uintptr_t>(d_parity) & 15) == 0 && k <= kMaxRaggedK;
   // one launch for every stripe's coding and every chunk's MD5 (k_files_md5):
-  // full stripes in place, last stripes from the tail arena after the pad copy
-  // (NXEC_FUSED_MD5=0: the separate launches, for A/B)
+  // full stripes in place, last stripes straight from their objects (the kernel
+  // also writes their zero-padded data chunks to the tail arena; NXEC_FUSED_MD5=0:
+  // pad copy + the separate launches, for A/B)
+  // NXEC_FILES_TAIL=0: last stripes through the pad copy into the tail arena
+  // first, then read from there (A/B of the in-kernel tail reads)
+  const char *tenv = std::getenv("NXEC_FILES_TAIL");
+  const bool tail_direct = !(tenv && tenv[0] == '0');
   const char *fenv = std::getenv("NXEC_FUSED_MD5");
   const bool want_fused = !(fenv && fenv[0] == '0') && d_md5 && ragged_ok && p <= kMaxRowsPerPass &&
                           k <= kFilesMd5MaxK;
-  std::vector<const uint8_t *> q_src;
+  std::vector<const uint8_t *> q_src, q_tsrc;
   std::vector<uint8_t *> q_dst, q_dig;
-  std::vector<int64_t> q_len;
+  std::vector<int64_t> q_len, q_trem;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
@@ -1029,6 +1034,8 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(M);
           q_dig.push_back(dig);
+          q_tsrc.push_back(nullptr);
+          q_trem.push_back(0);
         }
         if (dig) {
           for (int j = 0; j < k; j++) items.push_back({obj + (s * k + j) * M, M, dig + j * 16});
@@ -1054,11 +1061,13 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
           for (int j = 0; j < k; j++) ritems.push_back({td + j * cls, cl, dig + j * 16});
           for (int i = 0; i < p; i++) ritems.push_back({par + i * M, cl, dig + (k + i) * 16});
         }
-        if (want_fused) {
+        if (want_fused) {  // read from the object; the kernel writes the padded chunks to td
           for (int j = 0; j < k; j++) q_src.push_back(td + j * cls);
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(cl);
           q_dig.push_back(dig);
+          q_tsrc.push_back(tail_direct ? obj + nf * k * M : nullptr);
+          q_trem.push_back(lengths[o] - nf * k * M);
         }
         toff += k * cls;
       }
@@ -1088,9 +1097,9 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   }
   // fused: requests longest first (the slot planner packs them in this order)
   const bool fused = want_fused && full_aligned && !q_len.empty();
-  std::vector<const uint8_t *> f_src;
+  std::vector<const uint8_t *> f_src, f_tsrc;
   std::vector<uint8_t *> f_dst, f_dig;
-  std::vector<int64_t> f_len;
+  std::vector<int64_t> f_len, f_trem;
   if (fused) {
     const size_t R = q_len.size();
     std::vector<size_t> order(R);
@@ -1103,6 +1112,8 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
       f_dst.insert(f_dst.end(), q_dst.begin() + o * p, q_dst.begin() + (o + 1) * p);
       f_len.push_back(q_len[o]);
       f_dig.push_back(q_dig[o]);
+      f_tsrc.push_back(q_tsrc[o]);
+      f_trem.push_back(q_trem[o]);
     }
   }
   const std::vector<uint8_t> scratch_pad(fused ? 4096 : 0, 0);  // idle lanes' device line
@@ -1123,6 +1134,8 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
                       {slot_first.data(), slot_first.size() * sizeof(int32_t)},
                       {slot_reqs.data(), slot_reqs.size() * sizeof(int32_t)},
                       {wg_steps.data(), wg_steps.size() * sizeof(int32_t)},
+                      {f_tsrc.data(), f_tsrc.size() * sizeof(void *)},
+                      {f_trem.data(), f_trem.size() * sizeof(int64_t)},
                       {fsrc.data(), fsrc.size() * sizeof(void *)},
                       {fdst.data(), fdst.size() * sizeof(void *)},
                       {pads.data(), pads.size() * sizeof(PadChunks)},
@@ -1144,12 +1157,15 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   for (int i = 0; i < kTabs && !rc; i++)
     if (tabs[i].bytes) std::memcpy(slot->h + off[i], tabs[i].h, tabs[i].bytes);
   if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[kTabs], hipMemcpyHostToDevice, st), "tables H2D");
-  const int T0 = 8;  // the first eight tables belong to the fused launch
+  const int T0 = 10;  // the first ten tables belong to the fused launch
   auto dptr = [&](int i) { return slot->d + off[i + T0]; };
   if (fused) {
-    if (!rc)
+    // no pad copy: last stripes read their object and write the tail arena themselves
+    if (!rc && !tail_direct)
       rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
                              int64_t(pads.size()), pad_blocks, st);
+    fa.tail_src = reinterpret_cast<const uint8_t *const *>(slot->d + off[8]);
+    fa.tail_rem = reinterpret_cast<const int64_t *>(slot->d + off[9]);
     fa.src_ptrs = reinterpret_cast<const uint8_t *const *>(slot->d + off[0]);
     fa.dst_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[1]);
     fa.lens = reinterpret_cast<const int64_t *>(slot->d + off[2]);

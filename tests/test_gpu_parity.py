@@ -1266,6 +1266,72 @@ def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, 
     arena.free()
 
 
+@pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (6, 4, 4096), (20, 16, 2048), (5, 1, 1024)])
+def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, M):
+    """The one-launch write reads every last stripe straight from its object
+    (no pad copy): objects shorter than a stripe at every byte offset, chunk
+    lengths around the kernel's 256-byte steps (the last step's 16th lane
+    fetches the line after its own) and partial / empty data chunks.  Parity,
+    the zero-padded tail arena and every digest equal the separate launches
+    (pad copy + ragged + MD5 list) and the oracle / hashlib."""
+    import hashlib
+    p = n - k
+    rng = np.random.default_rng(7 * n + M)
+    lens = [1, 2, 15, 16, 17, 255, 256, 257, 1000]
+    for t in (1, 2, 3, 7):  # chunk lengths t*256 - 1 .. t*256 + 1: whole stripes and partial last chunks
+        for d in (-1, 0, 1):
+            cl = t * 256 + d
+            if cl <= M:
+                lens += [k * cl, k * cl - 5, (k - 1) * cl + 3]
+    lens += [int(x) for x in rng.integers(1, k * M, size=60)]
+    lens = [L for L in lens if 0 < L < k * M]
+    offs, pos = [], 0
+    for i, L in enumerate(lens):
+        pos += 1 + (i * 7) % 16  # every misalignment
+        offs.append(pos)
+        pos += L
+    host = rng.integers(0, 256, size=pos + 64, dtype=np.uint8)
+    arena = up(host)
+    total, tail_bytes = nxec.objects_layout(n, k, lens, M)
+    assert total == len(lens)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("NXEC_FUSED_MD5", mode)
+        par = nxec.DeviceBuffer(total * p * M)
+        par.memset(0)
+        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+        tail.memset(0xAB)
+        md5 = nxec.DeviceBuffer(total * n * 16)
+        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lens, M, par.ptr, tail.ptr, md5.ptr)
+        gpu_ctx.sync()
+        out[mode] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
+        for b in (par, tail, md5):
+            b.free()
+    (p1, t1, m1), (p0, t0, m0) = out["1"], out["0"]
+    assert np.array_equal(t1[:tail_bytes], t0[:tail_bytes])
+    assert np.array_equal(m1, m0)
+    toff = 0
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        assert (ns, nf) == (1, 0)
+        cls = (cl + 15) // 16 * 16
+        want = np.zeros(k * cl, dtype=np.uint8)
+        want[:L] = host[o:o + L]
+        chunks = want.reshape(k, cl)
+        got = t1[toff:toff + k * cls].reshape(k, cls)
+        assert np.array_equal(got[:, :cl], chunks) and not got[:, cl:].any(), (i, L)
+        assert np.array_equal(p1[i, :, :cl], p0[i, :, :cl]), (i, L)
+        if i % 7 == 0:
+            par_want = oracle.rs_encode(n, k, want, cl)
+            for r in range(p):
+                assert np.array_equal(p1[i, r, :cl], par_want[k + r]), (i, L, r)
+            for c in range(n):
+                data = chunks[c] if c < k else p1[i, c - k, :cl]
+                assert m1[i, c].tobytes().hex() == hashlib.md5(data.tobytes()).hexdigest(), (i, L, c)
+        toff += k * cls
+    arena.free()
+
+
 @pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 6000), (16, 12, 2048, 9000), (6, 4, 1024, 5000)])
 def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
     """More requests than the chip has slots (256 CUs x 16): the planner packs
