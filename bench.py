@@ -482,8 +482,8 @@ def wl_files(args, ctx, stream, rank):
               "byte_accounting": "data read + parity write + MD5 read of every chunk"}
     return Workload("files", "GiB/s multi-file write (encode+MD5), RS(10,4), 1 MiB max chunk, device-resident",
                     config, ops, [arena, par, tail, md5],
-                    "encode_objects: last-stripe pad copy + one k_files_md5 launch (NXEC_FUSED_MD5=0: gather + pad + "
-                    "ragged + MD5-list launches)", total)
+                    "encode_objects: one k_files_md5 launch, last stripes read from their objects (NXEC_FILES_TAIL=0: "
+                    "pad copy first; NXEC_FUSED_MD5=0: gather + pad + ragged + MD5-list launches)", total)
 
 
 CONFIG1 = ((6, 4, 1 << 20, "RS(4,2) read as (n,k)=(6,4), 4 MiB file, 1 MiB chunks"),
