@@ -686,6 +686,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     tail_state(0, len0, ltl, ljf, llast, lend);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
+      const bool wtl = __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
 #pragma unroll
       for (int j = 0; j < K; j++) {
         // a tail chunk's 16 bytes are read where they lie (global loads take
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         // first byte (the compute step shifts it into place), or the scratch
         // line once nothing of the tail is left
         const uint8_t *pj = sp[j] + off;
-        if (ltl)
+        if (wtl && ltl)
           pj = pj + 16 <= lend ? pj
                : pj < lend     ? reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pj) & ~uintptr_t(15))
                                : a.scratch + v * 16;
@@ -769,6 +770,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
       const bool tl = live && ctl != 0;
+      const bool wtc = __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
       uint8_t *rb = row + (step & 1) * buf_bytes;
       const int32_t pos = ct * kEncMd5Step + v * 16;
       const int64_t cls = (static_cast<int64_t>(ctl) + 15) / 16 * 16;
@@ -779,7 +781,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int j = 0; j < K; j += 2) {
         const int j1 = j + 1 < K ? j + 1 : j;
         u32x4 x0 = d[j], x1 = d[j1];
-        if (tl) {
+        if (wtc && tl) {
           const int32_t nv0 = valid_of(j, ctl, cjf, clast) - pos, nv1 = valid_of(j1, ctl, cjf, clast) - pos;
           if (nv0 < 16) x0 = tail_end(j, x0, nv0);
           if (nv1 < 16) x1 = tail_end(j1, x1, nv1);
