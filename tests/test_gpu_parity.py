@@ -1295,8 +1295,9 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
     total, tail_bytes = nxec.objects_layout(n, k, lens, M)
     assert total == len(lens)
     out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("NXEC_FUSED_MD5", mode)
+    for mode in ("1", "pad", "0"):  # tails read in the kernel / pad copy first (NXEC_FILES_TAIL=0) / separate launches
+        monkeypatch.setenv("NXEC_FUSED_MD5", "0" if mode == "0" else "1")
+        monkeypatch.setenv("NXEC_FILES_TAIL", "0" if mode == "pad" else "1")
         par = nxec.DeviceBuffer(total * p * M)
         par.memset(0)
         tail = nxec.DeviceBuffer(max(tail_bytes, 16))
@@ -1308,8 +1309,10 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
         for b in (par, tail, md5):
             b.free()
     (p1, t1, m1), (p0, t0, m0) = out["1"], out["0"]
-    assert np.array_equal(t1[:tail_bytes], t0[:tail_bytes])
-    assert np.array_equal(m1, m0)
+    for other in ("pad", "0"):
+        po, to, mo = out[other]
+        assert np.array_equal(t1[:tail_bytes], to[:tail_bytes]), other
+        assert np.array_equal(m1, mo), other
     toff = 0
     for i, (o, L) in enumerate(zip(offs, lens)):
         ns, nf, cl = nxec.object_layout(n, k, L, M)
@@ -1321,6 +1324,7 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
         got = t1[toff:toff + k * cls].reshape(k, cls)
         assert np.array_equal(got[:, :cl], chunks) and not got[:, cl:].any(), (i, L)
         assert np.array_equal(p1[i, :, :cl], p0[i, :, :cl]), (i, L)
+        assert np.array_equal(p1[i, :, :cl], out["pad"][0][i, :, :cl]), (i, L)
         if i % 7 == 0:
             par_want = oracle.rs_encode(n, k, want, cl)
             for r in range(p):
