@@ -39,7 +39,7 @@ def parse(argv=None):
                          "bench.py starts the N rank processes itself")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks only rendezvous (gloo), reduce and report")
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50, help="timed steps (default ~1 s of device time at the headline)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=14)
     ap.add_argument("--k", type=int, default=10)
