@@ -1017,19 +1017,28 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   std::vector<const uint8_t *> q_src, q_tsrc;
   std::vector<uint8_t *> q_dst, q_dig;
   std::vector<int64_t> q_len, q_trem;
+  // full stripes are read in place: 16-byte aligned objects (any object whose
+  // only stripe is its last one is read byte-wise, or padded, either way)
+  for (int o = 0; o < nobjects && full_aligned; o++)
+    full_aligned = (reinterpret_cast<uintptr_t>(d_objects[o]) & 15) == 0 || lengths[o] < int64_t(k) * M;
+  // the fused launch plans only its own tables; the separate launches only theirs
+  const bool fused = want_fused && full_aligned;
+  const bool sep = !fused;
+  const bool need_pads = sep || !tail_direct;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
     nxec_object_layout(n, k, lengths[o], M, &ns, &nf, &cl);
     const uint8_t *obj = d_objects[o];
-    full_aligned &= (reinterpret_cast<uintptr_t>(obj) & 15) == 0 || nf == 0;
     for (int64_t s = 0; s < ns; s++, g++) {
       uint8_t *par = d_parity ? d_parity + g * p * M : nullptr;
       uint8_t *dig = d_md5 ? d_md5 + g * n * 16 : nullptr;
       if (s < nf) {
-        for (int j = 0; j < k; j++) fsrc.push_back(obj + (s * k + j) * M);
-        for (int i = 0; i < p; i++) fdst.push_back(par + i * M);
-        if (want_fused) {
+        if (sep) {
+          for (int j = 0; j < k; j++) fsrc.push_back(obj + (s * k + j) * M);
+          for (int i = 0; i < p; i++) fdst.push_back(par + i * M);
+        }
+        if (fused) {
           for (int j = 0; j < k; j++) q_src.push_back(obj + (s * k + j) * M);
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(M);
@@ -1037,31 +1046,33 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
           q_tsrc.push_back(nullptr);
           q_trem.push_back(0);
         }
-        if (dig) {
+        if (sep && dig) {
           for (int j = 0; j < k; j++) items.push_back({obj + (s * k + j) * M, M, dig + j * 16});
           for (int i = 0; i < p; i++) items.push_back({par + i * M, M, dig + (k + i) * 16});
         }
       } else {  // last stripe (chunk_manager.cc:390-399)
         const int64_t cls = (cl + 15) / 16 * 16;
         uint8_t *td = d_tail + toff;
-        pads.push_back({obj + nf * k * M, td, lengths[o] - nf * k * M, cl, cls, k});
-        pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
-        pad_blocks += (cls / 16 * k + 256 * kPadVecs - 1) / (256 * kPadVecs);
-        if (p > 0 && !ragged_ok) {
+        if (need_pads) {
+          pads.push_back({obj + nf * k * M, td, lengths[o] - nf * k * M, cl, cls, k});
+          pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
+          pad_blocks += (cls / 16 * k + 256 * kPadVecs - 1) / (256 * kPadVecs);
+        }
+        if (sep && p > 0 && !ragged_ok) {
           ulist.push_back({td, par, cl, cls, M});
           uprefix.push_back(uprefix.back() + (cl + 15) / 16);
-        } else if (p > 0) {
+        } else if (sep && p > 0) {
           const uint32_t s_idx = static_cast<uint32_t>(ragged.size());
           ragged.push_back({td, par, cls, cls, M});
           stripe_tile0.push_back(static_cast<uint32_t>(tile_stripe.size()));
           const int64_t nt = (cls / 16 + 1023) / 1024;
           for (int64_t t = 0; t < nt; t++) tile_stripe.push_back(s_idx);
         }
-        if (dig) {
+        if (sep && dig) {
           for (int j = 0; j < k; j++) ritems.push_back({td + j * cls, cl, dig + j * 16});
           for (int i = 0; i < p; i++) ritems.push_back({par + i * M, cl, dig + (k + i) * 16});
         }
-        if (want_fused) {  // read from the object; the kernel writes the padded chunks to td
+        if (fused) {  // read from the object; the kernel writes the padded chunks to td
           for (int j = 0; j < k; j++) q_src.push_back(td + j * cls);
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(cl);
@@ -1096,7 +1107,6 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
     }
   }
   // fused: requests longest first (the slot planner packs them in this order)
-  const bool fused = want_fused && full_aligned && !q_len.empty();
   std::vector<const uint8_t *> f_src, f_tsrc;
   std::vector<uint8_t *> f_dst, f_dig;
   std::vector<int64_t> f_len, f_trem;
