@@ -298,7 +298,6 @@ bool digest_place_host(int64_t len, int nhash) {
 
 double digest_clock_ns() { return now_ns(CLOCK_MONOTONIC); }
 
-void digest_call_done(double start_ns) { (void)start_ns; }
 
 void digest_gpu_observe(int64_t len, double ms) {
   g_gpu_calls.fetch_add(1, std::memory_order_relaxed);

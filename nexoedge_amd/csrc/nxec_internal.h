@@ -20,9 +20,8 @@ void host_parallel_for(int n, const std::function<void(int)> &fn);
 bool digest_place_host(int64_t len, int nhash);
 // a GPU-placed call took `ms` end to end (feeds the placement's estimate)
 void digest_gpu_observe(int64_t len, double ms);
-// every call, on its way out (the placement's model of the callers' cycle)
+// CLOCK_MONOTONIC in ns (the GPU-placed call's latency)
 double digest_clock_ns();
-void digest_call_done(double start_ns);
 // the host-placed call: GPU coding, digests on the pool and the calling thread
 int encode_host_md5_host_digests(int len, int k, int rows, const unsigned char *coeffs,
                                  const unsigned char *const *data, unsigned char *const *coding,

@@ -2550,12 +2550,9 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
     return NXEC_OK;
   }
   // digests on the host pool or in the coding kernel (nxec_digest_place.cpp)
+  if (digest_place_host(len, (md5_data ? k : 0) + (md5_code ? rows : 0)))
+    return encode_host_md5_host_digests(len, k, rows, coeffs, data, coding, md5_data, md5_code);
   const double t_call = digest_clock_ns();
-  if (digest_place_host(len, (md5_data ? k : 0) + (md5_code ? rows : 0))) {
-    const int hrc = encode_host_md5_host_digests(len, k, rows, coeffs, data, coding, md5_data, md5_code);
-    digest_call_done(t_call);
-    return hrc;
-  }
   int rc = NXEC_OK;
   struct Observe {  // the GPU-placed call's latency, whichever way it returns
     int64_t len;
@@ -2563,7 +2560,6 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
     double t0;
     ~Observe() {
       if (rc == NXEC_OK) digest_gpu_observe(len, (digest_clock_ns() - t0) * 1e-6);
-      digest_call_done(t0);
     }
   } observe{len, rc, t_call};
   nxec_ctx_t *ctx = nullptr;
