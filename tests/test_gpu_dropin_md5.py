@@ -260,3 +260,54 @@ def test_void_drop_in_retries_after_an_injected_device_error(golden):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "retrying once on a fresh context" in r.stderr
     assert c["parity_sha256"] in r.stdout, r.stdout[-500:]
+
+
+AUTO_SWITCH = r"""
+import ctypes as C, hashlib, sys, threading
+sys.path.insert(0, {root!r})
+import numpy as np
+from nexoedge_amd import _lib, nxec
+import oracle
+lib = _lib.lib
+n, k, cs = 14, 10, 256 << 10
+enc = nxec.gen_rs_matrix(n, k)[k:]
+bad = []
+def worker(t, iters):
+    rng = np.random.default_rng(t)
+    for it in range(iters):
+        data = [rng.integers(0, 256, size=cs, dtype=np.uint8) for _ in range(k)]
+        outs, mi, mo = nxec.encode_host_md5(enc, data)
+        want = oracle.rs_encode(n, k, np.concatenate(data), cs)
+        for r in range(n - k):
+            if not (np.array_equal(outs[r], want[k + r]) and bytes(mo[r]) == hashlib.md5(want[k + r].tobytes()).digest()):
+                bad.append((t, it, r))
+        for j in range(k):
+            if bytes(mi[j]) != hashlib.md5(data[j].tobytes()).digest():
+                bad.append((t, it, 'd', j))
+def stats():
+    h, g, th = C.c_ulonglong(), C.c_ulonglong(), C.c_int()
+    lib.nxec_digest_place_stats(C.byref(h), C.byref(g), C.byref(th))
+    return h.value, g.value
+worker(99, 3)  # one caller: the pool
+h1, g1 = stats()
+ths = [threading.Thread(target=worker, args=(t, 12)) for t in range(6)]
+[x.start() for x in ths]
+[x.join() for x in ths]
+h2, g2 = stats()
+print("ONE", h1, g1, "MANY", h2 - h1, g2 - g1, "BAD", len(bad), flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_auto_placement_moves_many_callers_to_the_gpu():
+    """include/nxec.h §2, NXEC_DIGEST_PLACE=auto: a lone caller hashes on the
+    host pool; once more threads call than the crossover (here
+    NXEC_DIGEST_HOST_CALLERS=2, so 6 callers > 2H) the calls move to the
+    coding kernel -- every digest and parity byte right either way."""
+    r = _run(AUTO_SWITCH.format(root=ROOT), {"NXEC_DIGEST_HOST_CALLERS": "2", "NXEC_DIGEST_PLACE": "auto"}, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("ONE")][0].split()
+    one_h, one_g, many_h, many_g, nbad = int(line[1]), int(line[2]), int(line[4]), int(line[5]), int(line[7])
+    assert nbad == 0
+    assert one_h == 3 and one_g == 0, line
+    assert many_g > many_h and many_h + many_g == 72, line
