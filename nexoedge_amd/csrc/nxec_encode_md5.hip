@@ -771,6 +771,13 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       const bool ok = live && ct <= ctmax;
       const bool tl = live && ctl != 0;
       const bool wtc = __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
+      if (wtc) {
+        // wait for this step's loads here, in uniform control flow: a first
+        // use inside the per-lane tail branches below would be counted
+        // conservatively (vmcnt(0)) and drain the loads of the steps ahead
+#pragma unroll
+        for (int j = 0; j < K; j++) asm volatile("" ::"v"(d[j].x), "v"(d[j].y), "v"(d[j].z), "v"(d[j].w));
+      }
       uint8_t *rb = row + (step & 1) * buf_bytes;
       const int32_t pos = ct * kEncMd5Step + v * 16;
       const int64_t cls = (static_cast<int64_t>(ctl) + 15) / 16 * 16;
@@ -909,9 +916,11 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     w[14] = static_cast<uint32_t>(bits);
     w[15] = static_cast<uint32_t>(bits >> 32);
     md5_block(st, w);
-    uint8_t *out = reinterpret_cast<uint8_t *>(q[hr * rec + K + a.p]) + c * 16;
+    // a global (not flat) store: the digest may be unaligned
+    typedef __attribute__((address_space(1))) uint8_t g_u8;
+    g_u8 *out = reinterpret_cast<g_u8 *>(q[hr * rec + K + a.p] + static_cast<uint64_t>(c) * 16);
 #pragma unroll
-    for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));  // digest may be unaligned
+    for (int i = 0; i < 16; i++) out[i] = static_cast<uint8_t>(st[i / 4] >> (8 * (i % 4)));
     md5_init(st);
     if (hr + 1 < cnt) {
       hr++;
