@@ -15,21 +15,11 @@ namespace dev {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Streaming (nontemporal) 16-byte accesses: every source byte is read once and
-// every parity byte written once, so keep them from displacing the tables'
-// neighbours in L2/MALL.  Measured +2-3 % at RS(10,4) 1 MiB (tools/microbench/tune_mul.hip).
-__device__ __forceinline__ u32x4 ld_stream(const uint8_t *p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-}
-__device__ __forceinline__ void st_stream(uint8_t *p, u32x4 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(p));
-}
-
-// The same through global-address-space pointers: pointers read from tables
-// (per-request pointer tables, HBM or device-mapped host memory) are generic,
-// and generic (flat) accesses count in lgkmcnt as well as vmcnt -- every wait
-// for an LDS lookup then waited for the whole load ring too.  Global accesses
-// reach the same memory (no LDS / scratch aperture involved).
+// Global-address-space access: pointers read from tables (per-request
+// pointer tables, HBM or device-mapped host memory) are generic, and generic
+// (flat) accesses count in lgkmcnt as well as vmcnt -- every wait for an LDS
+// lookup then waited for the whole load ring too.  Global accesses reach the
+// same memory (no LDS / scratch aperture involved).
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
 __device__ __forceinline__ const g_u32x4 *gptr(const uint8_t *p) {
   return (const g_u32x4 *)(reinterpret_cast<uintptr_t>(p));
@@ -38,6 +28,13 @@ __device__ __forceinline__ g_u32x4 *gptr(uint8_t *p) { return (g_u32x4 *)(reinte
 __device__ __forceinline__ u32x4 ld_global(const uint8_t *p) { return *gptr(p); }
 __device__ __forceinline__ u32x4 ld_global_stream(const uint8_t *p) { return __builtin_nontemporal_load(gptr(p)); }
 __device__ __forceinline__ void st_global_stream(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, gptr(p)); }
+
+// Streaming (nontemporal) 16-byte accesses: every source byte is read once and
+// every parity byte written once, so keep them from displacing the tables'
+// neighbours in L2/MALL.  Measured +2-3 % at RS(10,4) 1 MiB (tools/microbench/tune_mul.hip).
+// Always global: the gather forms' table pointers would otherwise be flat.
+__device__ __forceinline__ u32x4 ld_stream(const uint8_t *p) { return ld_global_stream(p); }
+__device__ __forceinline__ void st_stream(uint8_t *p, u32x4 v) { st_global_stream(p, v); }
 
 // GF(2^8) product over the RS polynomial 0x11d (ISA-L gf_mul, ec_base.c:48-61)
 __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
