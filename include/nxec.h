@@ -610,6 +610,38 @@ int nxec_storage_classes_load(const char *path, nxec_storage_class *out, int max
 /* misc.repair_using_car of a proxy.ini (0 / 1 / true / false) into *car. */
 int nxec_proxy_repair_using_car(const char *path, int *car);
 
+/* ---------------------------------------------------------------------------
+ * 9. C++ surface ABI tripwire.  libnxec compiles RSCode, CodingOptions and
+ *    the Chunk / DecodingPlan / ByteBuffer code it runs against
+ *    the headers in nexoedge_amd/csrc/coding; a caller (the overlaid Nexoedge tree,
+ *    tools/overlay_reference.sh) compiles the inline half of the same types
+ *    against whatever headers its include graph reaches.  RSCode's public
+ *    one-argument constructor is inline (rs.hh): it records the caller's
+ *    sizes and offsets here and hands them to the exported constructor, which
+ *    throws std::invalid_argument on any difference, so CodingGenerator::
+ *    genCoding returns NULL instead of two layouts sharing one object
+ *    (reference coding_generator.hh:19-22 catches it the same way).  A TU
+ *    compiled against the reference's own rs.hh does not link at all: libnxec
+ *    exports no RSCode::RSCode(CodingOptions).
+ * ------------------------------------------------------------------------- */
+#define NXEC_CXX_ABI_VERSION 1u
+typedef struct nxec_cxx_abi {
+  uint32_t version; /* NXEC_CXX_ABI_VERSION of the header the caller saw */
+  uint32_t size_chunk, align_chunk;
+  uint32_t off_chunk_uuid, off_chunk_id, off_chunk_data, off_chunk_size, off_chunk_free, off_chunk_md5,
+      off_chunk_digest;
+  uint32_t size_uuid;
+  uint32_t size_coding_options;
+  uint32_t size_byte_buffer;
+  uint32_t size_decoding_plan;
+  uint32_t size_rscode;
+} nxec_cxx_abi;
+/* NXEC_OK when *caller equals libnxec's own layout, else NXEC_ERR_INVALID with
+ * the first differing field in nxec_last_error(). */
+int nxec_cxx_abi_check(const nxec_cxx_abi *caller);
+/* libnxec's own layout (what nxec_cxx_abi_check compares against) */
+void nxec_cxx_abi_self(nxec_cxx_abi *out);
+
 #ifdef __cplusplus
 }
 #endif

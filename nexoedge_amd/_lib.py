@@ -127,6 +127,8 @@ _PROTOS = {
     "nxec_digest_place_stats": (C.c_int, [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
     "nxec_storage_classes_load": (C.c_int, [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]),
     "nxec_proxy_repair_using_car": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),
+    "nxec_cxx_abi_check": (C.c_int, [vp]),
+    "nxec_cxx_abi_self": (None, [vp]),
     "nxec_reset_work_queues": (C.c_int, []),
     "nxec_debug_poison_next_queue_slot": (C.c_int, [C.c_uint32]),
     "nxec_pci_numa_node": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),

@@ -11,8 +11,46 @@
 #include <stdexcept>
 #include <vector>
 
-// rs.cc:11-30
-RSCode::RSCode(CodingOptions options) {
+extern "C" void nxec_cxx_abi_self(nxec_cxx_abi *out) {
+  if (out) *out = RSCode::callerAbi();  // compiled here: libnxec's own layout
+}
+
+extern "C" int nxec_cxx_abi_check(const nxec_cxx_abi *c) {
+  if (!c) return nxec::set_error(NXEC_ERR_INVALID, "nxec_cxx_abi_check: NULL layout");
+  const nxec_cxx_abi s = RSCode::callerAbi();
+  struct Field {
+    const char *name;
+    uint32_t nxec_cxx_abi::*m;
+  };
+  static const Field fields[] = {
+      {"version", &nxec_cxx_abi::version},
+      {"sizeof(Chunk)", &nxec_cxx_abi::size_chunk},
+      {"alignof(Chunk)", &nxec_cxx_abi::align_chunk},
+      {"offsetof(Chunk, fuuid)", &nxec_cxx_abi::off_chunk_uuid},
+      {"offsetof(Chunk, chunkId)", &nxec_cxx_abi::off_chunk_id},
+      {"offsetof(Chunk, data)", &nxec_cxx_abi::off_chunk_data},
+      {"offsetof(Chunk, size)", &nxec_cxx_abi::off_chunk_size},
+      {"offsetof(Chunk, freeData)", &nxec_cxx_abi::off_chunk_free},
+      {"offsetof(Chunk, md5)", &nxec_cxx_abi::off_chunk_md5},
+      {"offsetof(Chunk, digestData)", &nxec_cxx_abi::off_chunk_digest},
+      {"sizeof(Chunk::fuuid)", &nxec_cxx_abi::size_uuid},
+      {"sizeof(CodingOptions)", &nxec_cxx_abi::size_coding_options},
+      {"sizeof(ByteBuffer)", &nxec_cxx_abi::size_byte_buffer},
+      {"sizeof(DecodingPlan)", &nxec_cxx_abi::size_decoding_plan},
+      {"sizeof(RSCode)", &nxec_cxx_abi::size_rscode},
+  };
+  for (const Field &f : fields)
+    if (c->*f.m != s.*f.m)
+      return nxec::set_error(NXEC_ERR_INVALID,
+                             "C++ surface ABI mismatch: %s is %u in the caller, %u in libnxec (the caller's include "
+                             "graph reached other Chunk/coding headers than libnxec's; see tools/overlay_reference.sh)",
+                             f.name, c->*f.m, s.*f.m);
+  return NXEC_OK;
+}
+
+// rs.cc:11-30, after the layout check (include/nxec.h §9)
+RSCode::RSCode(CodingOptions options, const nxec_cxx_abi &callerLayout) {
+  if (nxec_cxx_abi_check(&callerLayout) != NXEC_OK) throw std::invalid_argument(nxec_last_error());
   const coding_param_t n = options.getN(), k = options.getK();
   if (n <= 0 || k <= 0 || n < k) throw std::invalid_argument("RS codes only support n>=k, n > 0, and k > 0");
   _options = options;

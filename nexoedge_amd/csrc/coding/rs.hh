@@ -4,6 +4,7 @@
 #ifndef NXEC_CODING_RS_HH
 #define NXEC_CODING_RS_HH
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "coding.hh"
@@ -11,7 +12,15 @@
 
 class RSCode : public Coding {
  public:
-  explicit RSCode(CodingOptions options);
+  // rs.hh:12.  Inline on purpose: it records the layout of Chunk,
+  // CodingOptions, ByteBuffer, DecodingPlan and RSCode as the *calling* TU
+  // sees them and the exported constructor below compares that with
+  // libnxec's own (include/nxec.h §9), throwing std::invalid_argument on a
+  // difference -- the case of a Nexoedge TU whose include graph reached other
+  // headers than the ones libnxec was built with.
+  RSCode(CodingOptions options) : RSCode(options, callerAbi()) {}
+  // rs.cc:11-30 plus the ABI check; throws std::invalid_argument
+  RSCode(CodingOptions options, const nxec_cxx_abi &callerLayout);
   ~RSCode() {}
 
   num_t getNumDataChunks();
@@ -37,6 +46,27 @@ class RSCode : public Coding {
                       void *stream = nullptr);
 
   const uint8_t *getEncodeMatrix() const { return _encodeMatrix; }
+
+  // the layout of the C++ surface as the TU that compiles this sees it
+  static nxec_cxx_abi callerAbi() {
+    nxec_cxx_abi a;
+    a.version = NXEC_CXX_ABI_VERSION;
+    a.size_chunk = sizeof(Chunk);
+    a.align_chunk = alignof(Chunk);
+    a.off_chunk_uuid = offsetof(Chunk, fuuid);
+    a.off_chunk_id = offsetof(Chunk, chunkId);
+    a.off_chunk_data = offsetof(Chunk, data);
+    a.off_chunk_size = offsetof(Chunk, size);
+    a.off_chunk_free = offsetof(Chunk, freeData);
+    a.off_chunk_md5 = offsetof(Chunk, md5);
+    a.off_chunk_digest = offsetof(Chunk, digestData);
+    a.size_uuid = sizeof(Chunk::fuuid);
+    a.size_coding_options = sizeof(CodingOptions);
+    a.size_byte_buffer = sizeof(ByteBuffer);
+    a.size_decoding_plan = sizeof(DecodingPlan);
+    a.size_rscode = sizeof(RSCode);
+    return a;
+  }
 
  private:
   bool carRepairFinalize(unsigned char *inputp[], num_t numInputChunks, length_t chunkSize, unsigned char *decodep[]);

@@ -104,7 +104,7 @@ def test_default_options_read_config_via_bridge():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("at_proxy", [1, 0])
-def test_unmodified_chunk_manager_car_repair(golden, at_proxy):
+def test_chunk_manager_flow_replica_car_repair(golden, at_proxy):
     """CAR single-failure repair with CAR taken from Config only (no setRepairUsingCAR
     call, as in the reference), at the proxy (accessGroupedChunks + RSCode::decode
     with G < k partials, chunk_manager.cc:1029,1141) and at an agent
@@ -123,7 +123,7 @@ def test_unmodified_chunk_manager_car_repair(golden, at_proxy):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("at_proxy", [1, 0])
-def test_unmodified_chunk_manager_conventional_repair(golden, at_proxy):
+def test_chunk_manager_flow_replica_conventional_repair(golden, at_proxy):
     """Same flows with repair_using_car = 0: k inputs and the plan's repair row,
     at the proxy (RSCode::decode) and at an agent (CodingUtils::encode with the
     proxy's matrix, agent.cc:339); fewer than k inputs are refused (rs.cc:133-136)."""
