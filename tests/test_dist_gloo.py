@@ -6,6 +6,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 from nexoedge_amd.dist import shard_range
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -106,22 +108,46 @@ def _bench(args, env_extra=None, timeout=240):
                           text=True, timeout=timeout)
 
 
-def test_bench_launches_ranks_itself():
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_launches_ranks_itself(world):
     """`bench.py --gpus N` without torch.distributed.run starts N rank
     processes (gloo rendezvous on 127.0.0.1) and prints rank 0's single line
-    with n_gpus = N (dry run: no GPU work)."""
+    with n_gpus = N (dry run: no GPU work); N = 8 is the driver's node."""
     import json
 
-    r = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1"])
+    r = _bench(["--gpus", str(world), "--dry-run", "--steps", "3", "--warmup", "1"])
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
-    assert abs(d["max_elapsed_s"] - 0.002) < 1e-9  # max over ranks, not rank 0's own value
+    assert d["n_gpus"] == world and d["ranks_seen"] == world and d["steps"] == 3
+    assert abs(d["max_elapsed_s"] - 0.001 * world) < 1e-9  # max over ranks, not rank 0's own value
 
 
 def test_bench_launcher_fails_when_a_rank_fails():
     r = _bench(["--gpus", "2", "--dry-run"], {"NXEC_DRY_RUN_FAIL_RANK": "1"})
     assert r.returncode != 0
     assert "rank 1 exited with status 3" in r.stderr
+
+
+def test_bench_under_torch_distributed_run_world8():
+    """The driver's own N = 8 launch: `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 ... bench.py --gpus 8`
+    (dry run: rendezvous, barrier, max-over-ranks and sums, one JSON line)."""
+    import json
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "8", "--dry-run", "--steps", "4", "--warmup", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["ranks_seen"] == 8 and abs(d["max_elapsed_s"] - 0.008) < 1e-9

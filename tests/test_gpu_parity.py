@@ -883,15 +883,18 @@ def test_encode_host_ex_pipelined(gpu_ctx, cs, threads):
     assert not errs, errs
 
 
-def test_group_two_contexts_host_and_device(gpu_ctx):
-    """nxec_group over two contexts on device 0 (the only one here): the
-    host-batch encode shards stripes across both, and device-resident shards
+@pytest.mark.parametrize("members", [2, 8])
+def test_group_contexts_host_and_device(gpu_ctx, members):
+    """nxec_group over `members` contexts on device 0 (the only one here; 8 is
+    the world of one MI355X node, each member with its own device thread): the
+    host-batch encode shards stripes across all, and device-resident shards
     encode + recover independently; bit-exact vs the oracle."""
-    n, k, cs, ns = 14, 10, 65536 + 16, 7
+    n, k, cs = 14, 10, 65536 + 16
+    ns = 3 * members + 1  # shard sizes differ by one
     p = n - k
-    g = nxec.Group([0, 0])
+    g = nxec.Group([0] * members)
     try:
-        assert len(g) == 2
+        assert len(g) == members
         hd = nxec.PinnedBuffer(ns * k * cs)
         hp = nxec.PinnedBuffer(ns * p * cs)
         data = [fill_bytes(k * cs, 5100 + s) for s in range(ns)]
@@ -905,10 +908,11 @@ def test_group_two_contexts_host_and_device(gpu_ctx):
         hd.free()
         hp.free()
         # device-resident shards, one buffer per group member
-        counts = [g.shard(ns, 2, i)[1] for i in range(2)]
+        counts = [g.shard(ns, members, i)[1] for i in range(members)]
+        starts = [sum(counts[:i]) for i in range(members)]
         bufs, hosts = [], []
         for i, c in enumerate(counts):
-            b, h = stripe_buffer(n, k, cs, cs, data[:c] if i == 0 else data[counts[0]:])
+            b, h = stripe_buffer(n, k, cs, cs, data[starts[i]:starts[i] + c])
             bufs.append(b)
             hosts.append(h)
         g.rs_encode(n, k, [b.ptr for b in bufs], cs, n * cs, cs, counts)
@@ -918,10 +922,12 @@ def test_group_two_contexts_host_and_device(gpu_ctx):
         gpu_ctx.sync()
         g.rs_recover(n, k, [1, 4, 11, 13], [b.ptr for b in bufs], cs, n * cs, cs, counts)
         assert [b.checksum() for b in bufs] == sums
-        got = bufs[1].download().reshape(counts[1], n, cs)
-        for s in range(counts[1]):
-            want = oracle.matmul(enc, list(data[counts[0] + s].reshape(k, cs)))
-            assert all(np.array_equal(got[s, k + r], want[r]) for r in range(p)), s
+        for i, b in enumerate(bufs):
+            got = b.download().reshape(counts[i], n, cs)
+            for s in range(counts[i]):
+                want = oracle.matmul(enc, list(data[starts[i] + s].reshape(k, cs)))
+                assert np.array_equal(got[s, :k], data[starts[i] + s].reshape(k, cs)), (i, s)
+                assert all(np.array_equal(got[s, k + r], want[r]) for r in range(p)), (i, s)
         for b in bufs:
             b.free()
     finally:
