@@ -111,6 +111,10 @@ int nxec_set_digest_placement(int mode);
 int nxec_digest_placement(void);
 /* calls placed on the host pool / the GPU so far, and the pool's threads */
 int nxec_digest_place_stats(unsigned long long *host_calls, unsigned long long *gpu_calls, int *host_threads);
+/* the auto placement's inputs: the process's CPU budget (the smallest cgroup
+ * quota from its own cgroup up, capped by the affinity mask; NXEC_DIGEST_CPUS
+ * overrides) and the crossover H in calling threads (NXEC_DIGEST_HOST_CALLERS) */
+int nxec_digest_place_params(double *cpu_budget, double *host_callers);
 
 /* ---------------------------------------------------------------------------
  * 2b. The boundary under the names of SURVEY §8b (thin forms of the above,
@@ -556,8 +560,14 @@ int nxec_host_range_mapped(const void *p, size_t bytes);
  *     chunk, marked on the Chunk itself) and RSCode::decode(isRepair) (the
  *     repaired regions) hash them in the same GPU kernel instead, and the
  *     regions' digests wait here, per calling thread, keyed by (pointer,
- *     length).  Each noting call clears the thread's table first; an entry is
- *     taken once; Chunk::release forgets its buffer's entry.
+ *     length), together with a 64-bit fingerprint of the bytes: a take is a hit
+ *     only on the noting thread, for the same length, and while the bytes
+ *     still have that fingerprint (a buffer freed with plain free() and handed
+ *     out again, or rewritten, is hashed afresh).  Each noting call clears the
+ *     thread's entries first; an entry is taken once; nxec_digest_forget (any
+ *     thread; Chunk::release calls it) drops the buffer's entry.  The marks
+ *     RSCode::encode leaves on Chunks hold while the thread's digest epoch is
+ *     unchanged: Chunk::allocateData and every freed Chunk buffer move it on.
  *     nxec_chunk_md5_mode: NXEC_CHUNK_MD5 = 0 (never; computeMD5 hashes on the
  *     host), 1 (default: RSCode::encode, whose n digests per stripe the GPU
  *     finishes sooner than one host thread hashing them in turn), 2 (also the
@@ -573,6 +583,9 @@ int nxec_digest_note(const void *p, int64_t len, const unsigned char *md5);
 /* 1 and the digest in md5[16] if (p, len) was noted on this thread (the entry is removed), else 0 */
 int nxec_digest_take(const void *p, int64_t len, unsigned char *md5);
 void nxec_digest_forget(const void *p);
+/* the calling thread's digest epoch, and moving it on */
+uint64_t nxec_digest_epoch(void);
+void nxec_digest_epoch_bump(void);
 
 /* ---------------------------------------------------------------------------
  * 7. Recovery and testing hooks.

@@ -122,8 +122,11 @@ _PROTOS = {
     "nxec_digest_note": (C.c_int, [vp, i64, vp]),
     "nxec_digest_take": (C.c_int, [vp, i64, vp]),
     "nxec_digest_forget": (None, [vp]),
+    "nxec_digest_epoch": (C.c_uint64, []),
+    "nxec_digest_epoch_bump": (None, []),
     "nxec_set_digest_placement": (C.c_int, [C.c_int]),
     "nxec_digest_placement": (C.c_int, []),
+    "nxec_digest_place_params": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "nxec_digest_place_stats": (C.c_int, [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]),
     "nxec_storage_classes_load": (C.c_int, [C.c_char_p, vp, C.c_int, C.POINTER(C.c_int)]),
     "nxec_proxy_repair_using_car": (C.c_int, [C.c_char_p, C.POINTER(C.c_int)]),

@@ -27,13 +27,19 @@
 //    produced the bytes (include/nxec.h §6b): RSCode::encode hashes all n
 //    chunks of the stripe in its kernel and marks each chunk's digest valid
 //    for exactly (data, size); RSCode::decode(isRepair) and, on request,
-//    CodingUtils::encode leave their outputs' digests in a per-thread table
-//    keyed by (pointer, length).  A marked digest is used once and only while
-//    the buffer is the one it was computed for: allocateData, copy, move (of
-//    the destination), release and reset drop the mark, and copyMeta never
-//    carries it.  The reference's sequences between the coding call and the
-//    hash write nothing to the chunks (chunk_manager.cc:99 -> :175,
-//    :1141 -> :1173, agent.cc:339 -> :342).  NXEC_CHUNK_MD5=0 disables the
+//    CodingUtils::encode leave their outputs' digests in a table keyed by
+//    (pointer, length) and checked against a fingerprint of the bytes at
+//    take time (nxec_digest.cpp).  A marked digest is used once and only
+//    while the buffer is the one it was computed for: allocateData, copy,
+//    move (of the destination), release and reset drop the mark, copyMeta
+//    never carries it, and the mark also lapses when the calling thread's
+//    digest epoch moves on (any Chunk::allocateData or freed Chunk buffer on
+//    that thread, include/nxec.h §6b).  The reference's sequences between the
+//    coding call and the hash write nothing to the chunks (chunk_manager.cc:99
+//    -> :175, :1141 -> :1173, agent.cc:339 -> :342).
+//    Rule for other callers: do not write new bytes into `data` between the
+//    coding call and computeMD5 (the mark cannot see a store); call
+//    allocateData, or dropDigest(), first.  NXEC_CHUNK_MD5=0 disables the
 //    cached digests; verifyMD5 always hashes.
 //
 // File uuids are boost::uuids::uuid when boost is available (the Nexoedge
@@ -100,9 +106,11 @@ struct Chunk {
   char chunkVersion[CHUNK_VERSION_MAX_LEN];  /**< chunk version number for revert */
   unsigned char md5[MD5_DIGEST_LENGTH];      /**< chunk md5 checksum */
   // md5 holds the digest the GPU computed for exactly these bytes: valid
-  // while data == digestData and size == digestSize (not in the reference)
+  // while data == digestData, size == digestSize and the calling thread's
+  // digest epoch is digestEpoch (not in the reference; see the top)
   const unsigned char *digestData;
   int digestSize;
+  uint64_t digestEpoch;
 
   Chunk() { reset(); }
   ~Chunk() { release(); }
@@ -127,6 +135,7 @@ struct Chunk {
   bool allocateData(int sizet, bool aligned = false) {
     if (sizet <= 0) return false;
     dropDigest();  // the caller is about to (re)write the bytes
+    nxec_digest_epoch_bump();  // ... and so may any other chunk of this thread
     if (data != NULL && size == sizet && freeData && !aligned) return true;
     unsigned char *datat = NULL;
     const size_t min = chunk_arena_min_bytes();
@@ -169,6 +178,7 @@ struct Chunk {
     freeData = src.freeData;
     digestData = src.digestData;
     digestSize = src.digestSize;
+    digestEpoch = src.digestEpoch;
     src.data = 0;
     src.freeData = false;
     src.dropDigest();
@@ -191,7 +201,7 @@ struct Chunk {
   bool computeMD5() {
     if (size <= 0) return false;
     if (data != NULL && nxec_chunk_md5_mode() > 0) {
-      if (digestData == data && digestSize == size) {
+      if (digestData == data && digestSize == size && digestEpoch == nxec_digest_epoch()) {
         dropDigest();  // used once
         return true;
       }
@@ -213,10 +223,12 @@ struct Chunk {
   void setDigestValid() {
     digestData = data;
     digestSize = size;
+    digestEpoch = nxec_digest_epoch();
   }
   void dropDigest() {
     digestData = NULL;
     digestSize = 0;
+    digestEpoch = 0;
   }
 
   // chunk.hh:158-164, kept as is (including its memcmp truthiness)

@@ -26,6 +26,7 @@
 // same bytes.
 #include <openssl/evp.h>
 #include <sched.h>
+#include <unistd.h>
 #include <time.h>
 
 #include <algorithm>
@@ -37,6 +38,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -67,27 +69,74 @@ int mode() {
   return m;
 }
 
-// CPUs this process may use: the cgroup quota (cpu.max, v2; cfs quota, v1)
-// when one is set, else the affinity mask
+// the cgroup directories holding this process's CPU quota, innermost first:
+// /proc/self/cgroup names the process's own (possibly nested) cgroup, and the
+// effective limit is the smallest quota on the way up to the root
+std::vector<std::string> cgroup_dirs(bool v2) {
+  std::vector<std::string> dirs;
+  FILE *f = std::fopen("/proc/self/cgroup", "r");
+  if (!f) return dirs;
+  char line[4096];
+  std::string rel;
+  while (std::fgets(line, sizeof(line), f)) {
+    std::string l(line);
+    while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+    const size_t a = l.find(':'), b = a == std::string::npos ? a : l.find(':', a + 1);
+    if (b == std::string::npos) continue;
+    const std::string ctrl = l.substr(a + 1, b - a - 1), path = l.substr(b + 1);
+    if (v2 ? (l.compare(0, 2, "0:") == 0 && ctrl.empty())
+           : (ctrl == "cpu" || ctrl.find("cpu,") == 0 || ctrl.find(",cpu,") != std::string::npos ||
+              (ctrl.size() > 4 && ctrl.compare(ctrl.size() - 4, 4, ",cpu") == 0))) {
+      rel = path;
+      break;
+    }
+  }
+  std::fclose(f);
+  if (rel.empty() || rel[0] != '/') rel = "/";
+  const std::string base = v2 ? "/sys/fs/cgroup" : "/sys/fs/cgroup/cpu";
+  for (std::string r = rel;;) {
+    dirs.push_back(base + (r == "/" ? "" : r));
+    if (r == "/" || r.empty()) break;
+    const size_t cut = r.find_last_of('/');
+    r = cut == 0 ? "/" : r.substr(0, cut);
+  }
+  return dirs;
+}
+
+// quota / period of one cgroup directory, or 0 when it sets none
+double cgroup_quota(const std::string &dir, bool v2) {
+  double cpus = 0;
+  if (v2) {
+    if (FILE *f = std::fopen((dir + "/cpu.max").c_str(), "r")) {
+      char q[32] = {0};
+      long per = 0;
+      if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
+        cpus = std::atof(q) / static_cast<double>(per);
+      std::fclose(f);
+    }
+  } else if (FILE *g = std::fopen((dir + "/cpu.cfs_quota_us").c_str(), "r")) {
+    long quota = -1, per = 0;
+    if (std::fscanf(g, "%ld", &quota) == 1 && quota > 0)
+      if (FILE *h = std::fopen((dir + "/cpu.cfs_period_us").c_str(), "r")) {
+        if (std::fscanf(h, "%ld", &per) == 1 && per > 0) cpus = static_cast<double>(quota) / static_cast<double>(per);
+        std::fclose(h);
+      }
+    std::fclose(g);
+  }
+  return cpus;
+}
+
+// CPUs this process may use: the smallest cgroup quota (cpu.max, v2; cfs
+// quota, v1) from the process's own cgroup up to the root, capped by the
+// affinity mask
 double cpu_budget() {
   double cpus = 0;
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
-  if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-    char q[32] = {0};
-    long per = 0;
-    if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
-      cpus = std::min(cpus > 0 ? cpus : 1e9, std::atof(q) / static_cast<double>(per));
-    std::fclose(f);
-  } else if (FILE *g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
-    long quota = -1, per = 0;
-    if (std::fscanf(g, "%ld", &quota) == 1 && quota > 0)
-      if (FILE *h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
-        if (std::fscanf(h, "%ld", &per) == 1 && per > 0)
-          cpus = std::min(cpus > 0 ? cpus : 1e9, static_cast<double>(quota) / static_cast<double>(per));
-        std::fclose(h);
-      }
-    std::fclose(g);
+  const bool v2 = access("/sys/fs/cgroup/cgroup.controllers", F_OK) == 0;
+  for (const std::string &d : cgroup_dirs(v2)) {
+    const double q = cgroup_quota(d, v2);
+    if (q > 0) cpus = std::min(cpus > 0 ? cpus : 1e9, q);
   }
   return cpus > 0 ? cpus : 1;
 }
@@ -118,6 +167,8 @@ class DigestHost {
   }
 
   int threads() const { return nthreads_; }
+  double cpus() const { return cpus_; }
+  double hostCallers() const { return host_callers_; }
 
   // Auto placement of a call hashing `bytes` in chunks of `len` (true: the
   // host pool, its bytes then reserved).  The pool is CPU-bound (~16 ms of
@@ -337,6 +388,13 @@ int nxec_set_digest_placement(int m) {
 }
 
 int nxec_digest_placement(void) { return nxec::mode(); }
+
+int nxec_digest_place_params(double *cpu_budget, double *host_callers) {
+  nxec::DigestHost &h = nxec::DigestHost::get();
+  if (cpu_budget) *cpu_budget = h.cpus();
+  if (host_callers) *host_callers = h.hostCallers();
+  return NXEC_OK;
+}
 
 int nxec_digest_place_stats(unsigned long long *host_calls, unsigned long long *gpu_calls, int *host_threads) {
   if (host_calls) *host_calls = nxec::g_host_calls.load();

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -56,7 +57,9 @@ struct Arena {
   size_t in_use = 0;                      // bytes handed out
   size_t cap = size_t(16) << 30;
   bool disabled = false;
-  bool no_device = false;  // hipHostMalloc said there is no device: stop asking
+  // hipHostMalloc said there is no device at all: stop asking (read without
+  // the lock, hence atomic; a bad current device on one thread is not that)
+  std::atomic<bool> no_device{false};
   Arena() {
     const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
     if (pages > 0 && psz > 0) cap = std::min(cap, static_cast<size_t>(pages) * static_cast<size_t>(psz) / 8);
@@ -80,7 +83,7 @@ int nxec_host_alloc(size_t bytes, void **p) {
   const int c = class_of(bytes == 0 ? 1 : bytes);
   Arena &a = arena();
   if (c < 0 || a.disabled) return nxec::set_error(NXEC_ERR_NOMEM, "nxec_host_alloc: %zu bytes not served", bytes);
-  if (a.no_device) return nxec::set_error(NXEC_ERR_NODEV, "nxec_host_alloc: no device");
+  if (a.no_device.load(std::memory_order_relaxed)) return nxec::set_error(NXEC_ERR_NODEV, "nxec_host_alloc: no device");
   const size_t cb = class_bytes(c);
   {
     std::lock_guard<std::mutex> lk(a.mu);
@@ -99,7 +102,7 @@ int nxec_host_alloc(size_t bytes, void **p) {
   if (e != hipSuccess || !blk) {
     (void)hipGetLastError();
     a.pinned -= cb;
-    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) a.no_device = true;
+    if (e == hipErrorNoDevice) a.no_device.store(true, std::memory_order_relaxed);
     return nxec::set_error(e == hipErrorNoDevice ? NXEC_ERR_NODEV : NXEC_ERR_NOMEM, "nxec_host_alloc: %s",
                            hipGetErrorString(e));
   }

@@ -25,6 +25,7 @@
 #include <openssl/evp.h>
 
 #include <atomic>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -272,6 +273,120 @@ static void moveInputs(int cs) {
   delete[] replies;
 }
 
+// A one-slot allocator that hands a freed block straight back (what glibc's
+// tcache does for a same-size malloc on one thread): it forces the recycled
+// address the stale-digest cases below need, whichever thread frees.
+struct RecyclingPool {
+  unsigned char *slot = nullptr;
+  unsigned char *alloc(size_t n) {
+    unsigned char *p = slot ? slot : static_cast<unsigned char *>(std::malloc(n));
+    slot = nullptr;
+    return p;
+  }
+  void release(unsigned char *p) { slot = p; }
+  ~RecyclingPool() { std::free(slot); }
+};
+
+static void md5_of(const unsigned char *p, int n, unsigned char *d) {
+  unsigned int dl = 16;
+  EVP_Digest(p, static_cast<size_t>(n), d, &dl, EVP_md5(), nullptr);
+}
+
+// Mode-2 digests of plain regions (include/nxec.h §6b) against a recycled
+// buffer: a digest noted on thread A for (p, cs), the buffer freed with plain
+// free() and handed out again at the same address and size on thread B with
+// new bytes, then Chunk::computeMD5 on A must hash the new bytes (round-3
+// advisor: container_manager.cc:241-252's ENC output is noted, never hashed,
+// freed by the caller).  And nxec_digest_forget from another thread drops A's entry.
+static void staleDigestAcrossThreads(int cs) {
+  if (nxec_chunk_md5_mode() < 1) return;
+  RecyclingPool pool;
+  unsigned char *buf = pool.alloc(cs);
+  fill(buf, cs, 901);
+  unsigned char dOld[16], dNew[16];
+  md5_of(buf, cs, dOld);
+  nxec_digest_clear();
+  CHECK(nxec_digest_note(buf, cs, dOld) == NXEC_OK, "note on A");
+  unsigned char *again = nullptr;
+  std::thread b([&] {
+    pool.release(buf);      // free() on B ...
+    again = pool.alloc(cs);  // ... and malloc of the same size hands it out again
+    fill(again, cs, 902);    // new bytes
+  });
+  b.join();
+  CHECK(again == buf, "recycled address");
+  md5_of(again, cs, dNew);
+  {
+    Chunk c;
+    c.data = again;
+    c.size = cs;
+    c.freeData = false;
+    CHECK(c.computeMD5() && std::memcmp(c.md5, dNew, 16) == 0 && std::memcmp(c.md5, dOld, 16) != 0,
+          "computeMD5 on A hashes the recycled buffer's new bytes, not the stale digest");
+  }
+  // the same bytes under a stale entry: the digest is right either way
+  CHECK(nxec_digest_note(again, cs, dNew) == NXEC_OK, "note again");
+  std::thread f([&] { nxec_digest_forget(again); });  // Chunk::freeBuffer on another thread
+  f.join();
+  unsigned char got[16];
+  CHECK(nxec_digest_take(again, cs, got) == 0, "forget from another thread drops A's entry");
+  pool.release(again);
+}
+
+// repairFile's tail (chunk_manager.cc:1137-1174) twice at one repairedData
+// address: run 1's decode notes both repaired regions, the PUT loop hashes
+// only the first (its bad_alloc exit at :1155-1158 leaves the loop), and
+// repairedData is freed; run 2 gets the same address back with other bytes
+// and a decode that notes nothing (NXEC_CHUNK_MD5 < 2, or the digest-less
+// path), so computeMD5 of region 1 must hash run 2's bytes.
+static void repairTailTwice(int cs) {
+  if (nxec_chunk_md5_mode() < 1) return;
+  RecyclingPool pool;
+  const int nrep = 2;
+  unsigned char *first = nullptr;
+  for (int run = 0; run < 2; run++) {
+    unsigned char *repairedData = pool.alloc(static_cast<size_t>(cs) * nrep);  // :1137
+    if (run == 0) first = repairedData;
+    else CHECK(repairedData == first, "run 2 reuses run 1's address");
+    for (int t = 0; t < nrep; t++) fill(repairedData + static_cast<size_t>(t) * cs, cs, 1000 + 10 * run + t);
+    if (run == 0) {  // what RSCode::decode(isRepair) leaves under NXEC_CHUNK_MD5=2 (rs.cc here)
+      nxec_digest_clear();
+      for (int t = 0; t < nrep; t++) {
+        unsigned char d[16];
+        md5_of(repairedData + static_cast<size_t>(t) * cs, cs, d);
+        nxec_digest_note(repairedData + static_cast<size_t>(t) * cs, cs, d);
+      }
+    }
+    const int hashed = run == 0 ? 1 : nrep;
+    for (int t = 0; t < hashed; t++) {  // :1168-1174
+      Chunk c;
+      c.size = cs;
+      c.data = repairedData + static_cast<size_t>(t) * cs;
+      CHECK(c.computeMD5() && md5_ok(c), "run %d repaired chunk %d md5 matches its bytes", run, t);
+      c.freeData = false;
+    }
+    pool.release(repairedData);  // free(repairedData) at the end of repairFile
+  }
+}
+
+// RSCode::encode's marks on the Chunks themselves lapse when the thread
+// allocates or frees chunk buffers before hashing (the rule in chunk.hh)
+static void chunkMarkLapses(int cs) {
+  if (nxec_chunk_md5_mode() < 1) return;
+  Chunk c;
+  c.allocateData(cs);
+  fill(c.data, cs, 1200);
+  std::memset(c.md5, 0xAB, 16);  // a digest that is not the bytes'
+  c.setDigestValid();
+  Chunk other;
+  other.allocateData(cs);  // another chunk buffer on this thread: the epoch moves on
+  CHECK(c.computeMD5() && md5_ok(c), "a mark from before an allocation is not trusted");
+  std::memset(c.md5, 0xAB, 16);
+  c.setDigestValid();
+  { Chunk tmp; tmp.allocateData(cs); }  // allocated and freed
+  CHECK(c.computeMD5() && md5_ok(c), "a mark from before a free is not trusted");
+}
+
 int main(int argc, char **argv) {
   const int cs = argc > 1 ? std::atoi(argv[1]) : (256 << 10);
   int dev = 0;
@@ -288,6 +403,9 @@ int main(int argc, char **argv) {
   }
   agentRepair(cs);
   moveInputs(cs);
+  staleDigestAcrossThreads(cs);
+  repairTailTwice(cs);
+  chunkMarkLapses(cs);
   std::printf("%s %d failures (%s)\n", g_fail ? "FAILED" : "PASSED", g_fail, g_gpu ? "gpu" : "cpu");
   return g_fail ? 1 : 0;
 }

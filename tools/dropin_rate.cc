@@ -18,6 +18,7 @@
 //
 // usage: dropin_rate [cs] [seconds] [all|agent|write] [threads,...]
 // Build: make tools   (build/dropin_rate)
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -56,10 +57,8 @@ int main(int argc, char **argv) {
       if (*p == ',') p++;
     }
   }
-  for (int threads : tlist0) {
-    if (agent_only) break;
-    for (int op = write_only ? 3 : 0; op < 4; op++) {  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode,
-                                                       // 3 writeFileStripe (encode + MD5 of every chunk + events)
+  // one timed leg of path `op` with `threads` callers; prints its line, returns GiB/s
+  auto leg = [&](int threads, int op, double secs) -> double {
       std::atomic<long> stripes{0};
       std::atomic<bool> ok{true};
       unsigned long long h0 = 0, g0 = 0, h1 = 0, g1 = 0;
@@ -137,7 +136,58 @@ int main(int argc, char **argv) {
                   bytes / dt / (1 << 30), 1e3 * dt * threads / static_cast<double>(stripes), nxec_chunk_md5_mode(),
                   place_names[nxec_digest_placement() & 3], h1 - h0, g1 - g0, dthreads, ok ? "true" : "false");
       std::fflush(stdout);
+      return bytes / dt / (1 << 30);
+  };
+  // DROPIN_PLACES=host,gpu,auto (write leg only): every placement of
+  // nxec_encode_host_md5's digests in one process, DROPIN_REPS rounds in
+  // rotating order after a warm-up leg (arena pinning and first-touch page
+  // faults land in the warm-up, not in whichever placement runs first), and
+  // per caller count the median of each plus auto / best.
+  const char *places_env = std::getenv("DROPIN_PLACES");
+  if (write_only && places_env) {
+    std::vector<int> places;
+    for (const char *p = places_env; *p;) {
+      places.push_back(std::strncmp(p, "gpu", 3) == 0 ? NXEC_DIGEST_GPU
+                       : std::strncmp(p, "host", 4) == 0 ? NXEC_DIGEST_HOST : NXEC_DIGEST_AUTO);
+      while (*p && *p != ',') p++;
+      if (*p == ',') p++;
     }
+    const int reps = std::getenv("DROPIN_REPS") ? std::atoi(std::getenv("DROPIN_REPS")) : 3;
+    double cpus = 0, hcallers = 0;
+    nxec_digest_place_params(&cpus, &hcallers);
+    nxec_set_digest_placement(NXEC_DIGEST_HOST);
+    leg(tlist0.empty() ? 1 : tlist0.back(), 3, 1.0);  // warm-up
+    for (int threads : tlist0) {
+      std::vector<std::vector<double>> got(places.size());
+      for (int r = 0; r < reps; r++)
+        for (size_t i = 0; i < places.size(); i++) {
+          const size_t pi = (i + r) % places.size();
+          nxec_set_digest_placement(places[pi]);
+          got[pi].push_back(leg(threads, 3, secs));
+        }
+      std::printf("{\"summary\": \"writeFileStripe per stripe, median of %d\", \"threads\": %d, "
+                  "\"cpu_budget\": %.1f, \"host_callers_H\": %.1f", reps, threads, cpus, hcallers);
+      double best = 0, autov = -1;
+      static const char *pn[3] = {"auto", "gpu", "host"};
+      for (size_t i = 0; i < places.size(); i++) {
+        std::vector<double> v = got[i];
+        std::sort(v.begin(), v.end());
+        const double med = v[v.size() / 2];
+        std::printf(", \"%s_GiB_s\": %.2f", pn[places[i] & 3], med);
+        if (places[i] == NXEC_DIGEST_AUTO) autov = med;
+        else best = std::max(best, med);
+      }
+      if (autov >= 0 && best > 0) std::printf(", \"auto_over_best\": %.3f", autov / best);
+      std::printf("}\n");
+      std::fflush(stdout);
+    }
+    delete code;
+    return 0;
+  }
+  for (int threads : tlist0) {
+    if (agent_only) break;
+    for (int op = write_only ? 3 : 0; op < 4; op++)  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode,
+      leg(threads, op, secs);                        // 3 writeFileStripe (encode + MD5 of every chunk + events)
   }
   if (write_only) {
     delete code;
