@@ -452,10 +452,39 @@ def wl_object(args, ctx, stream, rank):
                     config, ops, [obj, par, md5, chunks, out, cmd5, ok], "encode_object (fused k_mul_md5)", ns)
 
 
+# MD5 chain of one 256-byte step of one chunk (4 blocks), measured alone with
+# the fused kernel's barriers: ~9.8 ms per 4096 steps (role probes,
+# profiles/r02_encode_md5_role_probes.log) -- the floor of a slot's run
+MD5_STEP_US = 9.8e3 / 4096
+
+
+def files_longest_slot(n, k, M, lengths, cus=256, step=256):
+    """Steps of the longest slot of nxec_encode_objects' fused plan (the LPT of
+    plan_files_slots, nxec_encode_md5.hip, over every request: a file's full
+    stripes and its last stripe), and the request count."""
+    import heapq
+
+    reqs = []
+    for L in lengths:
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        reqs += [M] * nf + ([cl] if ns > nf else [])
+    steps = sorted(((r + step - 1) // step for r in reqs), reverse=True)
+    slots = cus * min(16, 256 // n)
+    if len(steps) <= slots:
+        return (max(steps) if steps else 0), len(reqs)
+    heap = [(0, g) for g in range(slots)]
+    for st in steps:
+        load, g = heapq.heappop(heap)
+        heapq.heappush(heap, (load + st, g))
+    return max(l for l, _ in heap), len(reqs)
+
+
 def wl_files(args, ctx, stream, rank):
     """Many files per call (nxec_encode_objects): 4096 files with sizes uniform
     in [1 B, 2*k*M] (full and ragged last stripes mixed) packed in one arena,
-    encode + MD5 of every chunk.  Bytes = user data + parity written + MD5 reads."""
+    encode + MD5 of every chunk.  Bytes = the kernel's HBM side, the write14
+    convention: data read once + parity written + the zero-padded last-stripe
+    data chunks written to the tail arena (the MD5 reads come out of LDS)."""
     import numpy as np
 
     n, k, M = args.n, args.k, args.chunk
@@ -472,18 +501,34 @@ def wl_files(args, ctx, stream, rank):
     ptrs = [arena.ptr + int(o) for o in offs[:-1]]
     user = sum(lengths)
     layouts = [nxec.object_layout(n, k, L, M) for L in lengths]
-    chunk_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts)
+    parity_bytes = sum((nf * M + (ns - nf) * cl) * p for ns, nf, cl in layouts)
+    # NXEC_OBJECTS_TAIL_INPLACE (a batching ChunkManager sends whole chunks
+    # from the object, as it does for full stripes): of each last stripe only
+    # the partial data chunk is written, zero-padded, to the tail arena
+    tail_written = sum((cl + 15) // 16 * 16 for (ns, nf, cl), L in zip(layouts, lengths)
+                       if ns > nf and (L - nf * k * M) % cl)
+    longest, nreq = files_longest_slot(n, k, M, lengths)
     ops = [("encode_objects_md5",
-            lambda i: ctx.encode_objects(n, k, ptrs, lengths, M, par.ptr, tail.ptr, md5.ptr, stream),
-            user + 2 * chunk_bytes * p // n + chunk_bytes)]
+            lambda i: ctx.encode_objects(n, k, ptrs, lengths, M, par.ptr, tail.ptr, md5.ptr, stream,
+                                         flags=nxec.OBJECTS_TAIL_INPLACE),
+            user + parity_bytes + tail_written)]
     config = {"workload": f"{len(lengths)} files, sizes uniform in [1 B, {2 * k} MiB], RS({n},{k}) {M >> 10} KiB max "
                           f"chunks ({total} stripes, {user / 2**30:.1f} GiB user data): encode + MD5 of all chunks",
-              "files": len(lengths), "stripes": total, "user_bytes": user,
-              "byte_accounting": "data read + parity write + MD5 read of every chunk"}
+              "files": len(lengths), "stripes": total, "user_bytes": user, "requests": nreq,
+              "tail": "nxec_encode_objects_ex(NXEC_OBJECTS_TAIL_INPLACE): whole last-stripe data chunks stay in "
+                      "their objects, the partial one is written zero-padded",
+              "byte_accounting": "HBM side, the write14 convention: data read + parity written + tail-arena "
+                                 f"writes ({user / 2**30:.1f} + {parity_bytes / 2**30:.1f} + "
+                                 f"{tail_written / 2**30:.1f} GiB); the MD5 of every chunk reads LDS",
+              "md5_chain_floor": {"longest_slot_steps": longest, "us_per_step": round(MD5_STEP_US, 3),
+                                  "ms": round(longest * MD5_STEP_US / 1e3, 2),
+                                  "note": "one lane's MD5 chain per chunk, a slot's requests back to back: the "
+                                          "longest slot's 256-byte steps x the bare chain's step time "
+                                          "(profiles/r02_encode_md5_role_probes.log)"}}
     return Workload("files", "GiB/s multi-file write (encode+MD5), RS(10,4), 1 MiB max chunk, device-resident",
                     config, ops, [arena, par, tail, md5],
-                    "encode_objects: one k_files_md5 launch, last stripes read from their objects (NXEC_FILES_TAIL=0: "
-                    "pad copy first; NXEC_FUSED_MD5=0: gather + pad + ragged + MD5-list launches)", total)
+                    "encode_objects_ex(TAIL_INPLACE): one k_files_md5 launch, last stripes read from their objects, "
+                    "only their partial data chunks written to the tail arena", total)
 
 
 CONFIG1 = ((6, 4, 1 << 20, "RS(4,2) read as (n,k)=(6,4), 4 MiB file, 1 MiB chunks"),

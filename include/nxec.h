@@ -370,6 +370,22 @@ int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int6
 int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
                         const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
                         unsigned char *d_tail, unsigned char *d_md5, void *stream);
+/* The same with flags.  NXEC_OBJECTS_TAIL_INPLACE: a batching ChunkManager
+ * that sends every chunk from where it lies (the full stripes' data chunks
+ * are read in place already) needs only one data chunk of a last stripe
+ * materialised: with cl = last_chunk_size and r = the object's bytes past its
+ * full stripes, chunk j < r / cl is the object's bytes at
+ * nf*k*M + j*cl (whole, in place), chunk j = r / cl < k -- when r % cl != 0 --
+ * holds r % cl object bytes and is written zero-padded to its tail-arena
+ * slot (same layout as above), and chunks past it are all zero bytes.
+ * Parity and digests are those of the zero-padded stripe, as without the
+ * flag; tail-arena slots of whole and all-zero chunks are left unspecified
+ * (the one-launch path leaves them alone: k_files_md5 then writes ~1/k of
+ * the tail bytes). */
+#define NXEC_OBJECTS_TAIL_INPLACE 1
+int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
+                           const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
+                           unsigned char *d_tail, unsigned char *d_md5, int flags, void *stream);
 
 /* Host-inclusive form of nxec_encode_object: the object, parity
  * ([nstripes][n-k][M]) and digests ([nstripes][n][16], NULL = skip) are in

@@ -72,6 +72,7 @@ _PROTOS = {
     "nxec_encode_object_host": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, i64]),
     "nxec_objects_layout": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_objects": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, i64, vp, vp, vp, vp]),
+    "nxec_encode_objects_ex": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
     "nxec_decode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp]),
     "nxec_decode_object_ex": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, i64, vp, vp, vp]),
     "nxec_agent_encode_batch": (C.c_int, [vp, vp, C.c_int, i64, i64]),

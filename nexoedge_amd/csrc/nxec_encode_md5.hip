@@ -587,7 +587,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 // bytes past the chunk's end masked off) and starts the next chain at once.
 // A lane past its request's end in that request's last step re-reads its
 // last in-bounds vector, stores to scratch and leaves its LDS row alone.
-template <int K>
+// PROBE (design probes only, K = 10, NXEC_FM_PROBE; outputs are NOT valid),
+// as k_mul_md5's: bit 0 no MD5 rounds, bit 1 no table lookups, bit 2 no
+// global loads or stores.
+template <int K, int PROBE = 0>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = K + a.p;
@@ -703,7 +706,10 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         // object at any 16-byte offset, a tail at any byte) shares its
         // boundary lines between consecutive steps; streaming loads fetched
         // them once per step
-        if (a.cached_loads)
+        if (PROBE & 4)  // no HBM traffic: a value the compiler cannot fold
+          d[j] = u32x4{static_cast<uint32_t>(reinterpret_cast<uintptr_t>(pj)), static_cast<uint32_t>(lt),
+                       static_cast<uint32_t>(j), static_cast<uint32_t>(v)};
+        else if (a.cached_loads)
           d[j] = dev::ld_global(pj);
         else
           d[j] = dev::ld_global_stream(pj);
@@ -792,16 +798,22 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           const int32_t nv0 = valid_of(j, ctl, cjf, clast) - pos, nv1 = valid_of(j1, ctl, cjf, clast) - pos;
           if (nv0 < 16) x0 = tail_end(j, x0, nv0);
           if (nv1 < 16) x1 = tail_end(j1, x1, nv1);
-          if (ok) {  // the zero-padded data chunks into the tail arena
-            dev::st_global_stream(ctd + j * cls + pos, x0);
-            if (j + 1 < K) dev::st_global_stream(ctd + j1 * cls + pos, x1);
+          if (ok) {  // the zero-padded data chunks into the tail arena (in place: only the partial one)
+            const bool part0 = j == static_cast<int>(cjf) && clast != 0, part1 = j1 == static_cast<int>(cjf) && clast != 0;
+            if (!(PROBE & 4) && (!a.tail_partial_only || part0)) dev::st_global_stream(ctd + j * cls + pos, x0);
+            if (!(PROBE & 4) && j + 1 < K && (!a.tail_partial_only || part1))
+              dev::st_global_stream(ctd + j1 * cls + pos, x1);
           }
         }
         if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
           *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = x0;
           if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = x1;
         }
-        lookup_pair(j, j + 1 < K, x0, x1, acc);
+        if (PROBE & 2) {
+          if (j == 0) acc[0] = x0.x, acc[5] = x0.y, acc[10] = x0.z, acc[15] = x0.w;
+        } else {
+          lookup_pair(j, j + 1 < K, x0, x1, acc);
+        }
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
       }
@@ -812,7 +824,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int r = 0; r < kMaxRowsPerPass; r++) {
         if (r < a.p) {  // wave-uniform
           const u32x4 pv{o[r][0], o[r][1], o[r][2], o[r][3]};
-          dev::st_global_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
+          if (!(PROBE & 4)) dev::st_global_stream(ok ? dp[r] + off : a.scratch + 256 * (r + 1) + v * 16, pv);
           if (ok) *reinterpret_cast<u32x4 *>(rb + (K + r) * kEmRow) = pv;
         }
       }
@@ -884,8 +896,13 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   auto proc = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
     if (!live) return;
     if (ht < hT - 1) {
+      if (PROBE & 1) {
 #pragma unroll
-      for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+        for (int i = 0; i < kEncMd5Step / 4; i++) st[i & 3] ^= m[i];
+      } else {
+#pragma unroll
+        for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+      }
       ht++;
       return;
     }
@@ -959,6 +976,8 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int
   return {{&k_files_md5<Ks + 1>...}};
 }
 const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+const FmKernel kFmProbe[8] = {&k_files_md5<10, 0>, &k_files_md5<10, 1>, &k_files_md5<10, 2>, &k_files_md5<10, 3>,
+                              &k_files_md5<10, 4>, &k_files_md5<10, 5>, &k_files_md5<10, 6>, &k_files_md5<10, 7>};
 
 using GmKernel = void (*)(const GatherMd5Args);
 template <bool HSRC, int... Ks>
@@ -1089,47 +1108,59 @@ void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cu
   S = std::max<int64_t>(S, 1);
   const int64_t lds_free = kEmLds - int64_t(k) * 1024 - 2 * S * nh * kEmRow;
   const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 4) * 8));
-  std::vector<std::vector<int32_t>> lists(static_cast<size_t>(G));
+  // slot of every request; loads and list lengths per slot
+  std::vector<int32_t> slot_of(static_cast<size_t>(R));
   std::vector<int64_t> load(static_cast<size_t>(G), 0);
-  if (G == R) {
-    for (int64_t r = 0; r < R; r++) {
-      lists[static_cast<size_t>(r)].push_back(static_cast<int32_t>(r));
-      load[static_cast<size_t>(r)] = steps(lens[static_cast<size_t>(r)]);
-    }
-  } else {
-    // longest request first into the least loaded slot (LPT); a slot whose
-    // list fills the LDS request table takes no more; when every slot is
-    // full a new one opens (a second wave of workgroups)
-    typedef std::pair<int64_t, int64_t> Item;  // (load, slot)
-    std::priority_queue<Item, std::vector<Item>, std::greater<Item>> heap;
-    for (int64_t g = 0; g < G; g++) heap.push(Item(0, g));
-    for (int64_t r = 0; r < R; r++) {
-      int64_t g = -1;
-      while (!heap.empty()) {
-        const Item it = heap.top();
-        heap.pop();
-        if (static_cast<int64_t>(lists[static_cast<size_t>(it.second)].size()) < Lmax) {
-          g = it.second;
-          break;
-        }
-      }
-      if (g < 0) {
-        g = G++;
-        lists.emplace_back();
-        load.push_back(0);
-      }
-      lists[static_cast<size_t>(g)].push_back(static_cast<int32_t>(r));
-      load[static_cast<size_t>(g)] += steps(lens[static_cast<size_t>(r)]);
-      heap.push(Item(load[static_cast<size_t>(g)], g));
-    }
+  std::vector<int32_t> cnt(static_cast<size_t>(G), 0);
+  // longest request first into the least loaded slot (LPT; ties: lowest
+  // slot).  The requests come longest first, so the first G of them land one
+  // per empty slot in order; the rest go through a heap of (load, slot).  A
+  // slot whose list fills the LDS request table takes no more; when every
+  // slot is full a new one opens (a second wave of workgroups).
+  const int64_t first = std::min(R, G);
+  for (int64_t r = 0; r < first; r++) {
+    slot_of[static_cast<size_t>(r)] = static_cast<int32_t>(r);
+    load[static_cast<size_t>(r)] = steps(lens[static_cast<size_t>(r)]);
+    cnt[static_cast<size_t>(r)] = 1;
   }
-  slot_first.assign(1, 0);
-  slot_reqs.clear();
+  if (R > G) {
+    typedef std::pair<int64_t, int64_t> Item;  // (load, slot); a min-heap via std::greater
+    std::vector<Item> heap;
+    heap.reserve(static_cast<size_t>(G));
+    for (int64_t g = 0; g < G; g++)
+      if (cnt[static_cast<size_t>(g)] < Lmax) heap.push_back(Item(load[static_cast<size_t>(g)], g));
+    std::make_heap(heap.begin(), heap.end(), std::greater<Item>());
+    for (int64_t r = G; r < R; r++) {
+      int64_t g = -1;
+      if (!heap.empty()) {
+        std::pop_heap(heap.begin(), heap.end(), std::greater<Item>());
+        g = heap.back().second;
+        heap.pop_back();
+      } else {
+        g = static_cast<int64_t>(load.size());
+        load.push_back(0);
+        cnt.push_back(0);
+      }
+      slot_of[static_cast<size_t>(r)] = static_cast<int32_t>(g);
+      load[static_cast<size_t>(g)] += steps(lens[static_cast<size_t>(r)]);
+      if (++cnt[static_cast<size_t>(g)] < Lmax) {  // full slots leave the heap for good
+        heap.push_back(Item(load[static_cast<size_t>(g)], g));
+        std::push_heap(heap.begin(), heap.end(), std::greater<Item>());
+      }
+    }
+    G = static_cast<int64_t>(load.size());
+  }
+  // slot lists in request order (a counting sort by slot)
+  slot_first.assign(static_cast<size_t>(G) + 1, 0);
   int64_t maxl = 1;
-  for (const auto &l : lists) {
-    slot_reqs.insert(slot_reqs.end(), l.begin(), l.end());
-    slot_first.push_back(static_cast<int32_t>(slot_reqs.size()));
-    maxl = std::max<int64_t>(maxl, static_cast<int64_t>(l.size()));
+  for (int64_t g = 0; g < G; g++) {
+    slot_first[static_cast<size_t>(g) + 1] = slot_first[static_cast<size_t>(g)] + cnt[static_cast<size_t>(g)];
+    maxl = std::max<int64_t>(maxl, cnt[static_cast<size_t>(g)]);
+  }
+  slot_reqs.assign(static_cast<size_t>(R), 0);
+  {
+    std::vector<int32_t> fill(slot_first.begin(), slot_first.end() - 1);
+    for (int64_t r = 0; r < R; r++) slot_reqs[static_cast<size_t>(fill[static_cast<size_t>(slot_of[static_cast<size_t>(r)])]++)] = static_cast<int32_t>(r);
   }
   const int64_t nwg = (G + S - 1) / S;
   wg_steps.assign(static_cast<size_t>(nwg), 0);
@@ -1160,7 +1191,10 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
   const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
-  hipLaunchKernelGGL(kFm[a.k - 1], dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
+  FmKernel fn = kFm[a.k - 1];
+  if (const char *e = std::getenv("NXEC_FM_PROBE"))
+    if (a.k == 10) fn = kFmProbe[std::atoi(e) & 7];
+  hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? NXEC_OK : set_error(NXEC_ERR_HIP, "launch k_files_md5: %s", hipGetErrorString(e));

@@ -269,6 +269,10 @@ struct FilesMd5Args {
   // next multiple of 16, to src_ptrs[s*k + j] (the tail arena).
   const uint8_t *const *tail_src;
   const int64_t *tail_rem;
+  // NXEC_OBJECTS_TAIL_INPLACE: of a last stripe's data chunks only the
+  // partial one (zero-padded) is written to the tail arena; the whole ones
+  // stay where they are in the object, the all-zero ones are not written
+  int32_t tail_partial_only;
 };
 // Slot plan for `lens` (descending): fills slot_first / slot_reqs / wg_steps
 // and the args' nslots / slots_per_group / max_list.  NXEC_FILES_PACK=0 gives

@@ -965,7 +965,24 @@ int nxec_objects_layout(int n, int k, int nobjects, const int64_t *lengths, int6
 int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
                         const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
                         unsigned char *d_tail, unsigned char *d_md5, void *stream) {
+  return nxec_encode_objects_ex(ctx, n, k, nobjects, d_objects, lengths, max_chunk_size, d_parity, d_tail, d_md5, 0,
+                                stream);
+}
+
+int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
+                           const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
+                           unsigned char *d_tail, unsigned char *d_md5, int flags, void *stream) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  if (flags & ~NXEC_OBJECTS_TAIL_INPLACE) return set_error(NXEC_ERR_INVALID, "nxec_encode_objects_ex: flags %d", flags);
+  // NXEC_TIMING=1: the host side's share of the call on stderr (planning, tables, launch, wait)
+  static const bool timing = [] {
+    const char *e = std::getenv("NXEC_TIMING");
+    return e && e[0] == '1';
+  }();
+  const auto th0 = std::chrono::steady_clock::now();
+  auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+  };
   int64_t total = 0, tail_total = 0;
   int rc = nxec_objects_layout(n, k, nobjects, lengths, max_chunk_size, &total, &tail_total);
   if (rc) return rc;
@@ -1160,6 +1177,7 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
   size_t off[kTabs + 1] = {0};
   for (int i = 0; i < kTabs; i++) off[i + 1] = off[i] + (tabs[i].bytes + 15) / 16 * 16;
   Slot *slot = nullptr;
+  const double t_plan = timing ? ms_since(th0) : 0;
   rc = acquire_slot(ctx, std::max<size_t>(off[kTabs], 16), &slot);
   if (rc) return rc;
   // the slot's staging may still be in use by an earlier call on its own stream
@@ -1186,9 +1204,14 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
     fa.wg_steps = reinterpret_cast<const int32_t *>(slot->d + off[7]);
     fa.k = k;
     fa.p = p;
+    fa.tail_partial_only = (flags & NXEC_OBJECTS_TAIL_INPLACE) && tail_direct ? 1 : 0;
     std::memcpy(fa.coef, prow, size_t(p) * k);
     if (!rc) rc = launch_files_md5(fa, ctx->num_cus, st);
+    const double t_launch = timing ? ms_since(th0) : 0;
     const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
+    if (timing)
+      std::fprintf(stderr, "nxec_encode_objects: %d objects, %zu requests: plan %.3f ms, tables + launch %.3f ms, "
+                   "wait %.3f ms\n", nobjects, f_len.size(), t_plan, t_launch - t_plan, ms_since(th0) - t_launch);
     release_slot(ctx, slot);
     return rc ? rc : rc2;
   }

@@ -81,6 +81,7 @@ def decode_matrix(n: int, k: int, input_ids: Sequence[int], targets: Sequence[in
 
 
 LAYOUT_RECOVER_HEAVY = 1
+OBJECTS_TAIL_INPLACE = 1  # nxec_encode_objects_ex: only the partial last-stripe chunk to the tail arena
 
 
 def batch_layout(n: int, length: int, flags: int = 0):
@@ -461,12 +462,15 @@ class Context:
                                      C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_object")
 
     def encode_objects(self, n: int, k: int, objects: Sequence[int], lengths: Sequence[int], max_chunk_size: int,
-                       parity: int, tail=None, md5=None, stream=None) -> None:
+                       parity: int, tail=None, md5=None, stream=None, flags: int = 0) -> None:
+        """nxec_encode_objects_ex; flags = OBJECTS_TAIL_INPLACE writes only each
+        last stripe's partial data chunk to the tail arena (include/nxec.h)."""
         ptrs = (C.c_void_p * max(len(objects), 1))(*[int(o) if o else None for o in objects])
         ln = np.ascontiguousarray(np.asarray(list(lengths), dtype=np.int64))
-        check(lib.nxec_encode_objects(C.c_void_p(self.ptr), n, k, len(ln), ptrs, C.c_void_p(ln.ctypes.data),
-                                      max_chunk_size, C.c_void_p(int(parity)), C.c_void_p(int(tail) if tail else None),
-                                      C.c_void_p(int(md5) if md5 else None), stream), "nxec_encode_objects")
+        check(lib.nxec_encode_objects_ex(C.c_void_p(self.ptr), n, k, len(ln), ptrs, C.c_void_p(ln.ctypes.data),
+                                         max_chunk_size, C.c_void_p(int(parity)),
+                                         C.c_void_p(int(tail) if tail else None),
+                                         C.c_void_p(int(md5) if md5 else None), flags, stream), "nxec_encode_objects")
 
     def encode_object_host(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int,
                            md5=None, batch_stripes: int = 0) -> None:

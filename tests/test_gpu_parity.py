@@ -1398,3 +1398,66 @@ def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
             toff += k * ((cl + 15) // 16 * 16)
         g += ns
     arena.free()
+
+
+@pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 700), (14, 10, 65536, 300), (6, 4, 1000 * 16, 200),
+                                          (20, 16, 2048, 5000)])
+def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
+    """NXEC_OBJECTS_TAIL_INPLACE (include/nxec.h): parity and every digest equal
+    the default call's; each last stripe's partial data chunk is in its tail
+    slot, zero-padded; whole data chunks are the object's bytes in place (their
+    digests equal hashlib's of those bytes), all-zero ones are zeros (digest of
+    cl zero bytes), and the one-launch path writes no other tail slot."""
+    import hashlib
+    p = n - k
+    rng = np.random.default_rng(3 * nfiles + k)
+    lengths = [int(x) for x in rng.integers(1, 2 * k * M + 1, size=nfiles)]
+    lengths[:6] = [1, k * M, k * M + 1, 2 * k * M - 1, 5 * M, 3 * k * 257]  # edge cases, even tails
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    offs, pos = [], 0
+    for L in lengths:
+        offs.append(pos)
+        pos += (L + 15) // 16 * 16
+    host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
+    arena = up(host)
+    out = {}
+    for flags in (0, nxec.OBJECTS_TAIL_INPLACE):
+        par = nxec.DeviceBuffer(total * p * M)
+        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+        tail.memset(0xAB)
+        md5 = nxec.DeviceBuffer(total * n * 16)
+        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr,
+                               flags=flags)
+        out[flags] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
+        for b in (par, tail, md5):
+            b.free()
+    (p0, t0, m0), (p1, t1, m1) = out[0], out[nxec.OBJECTS_TAIL_INPLACE]
+    assert np.array_equal(m0, m1)
+    g, toff = 0, 0
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        for s in range(ns):
+            cs = M if s < nf else cl
+            assert np.array_equal(p0[g + s, :, :cs], p1[g + s, :, :cs]), (i, s)
+        if ns > nf:
+            cls = (cl + 15) // 16 * 16
+            r = L - nf * k * M
+            jf, part = r // cl, r % cl
+            slots = t1[toff:toff + k * cls].reshape(k, cls)
+            base = o + nf * k * M
+            for j in range(k):
+                if j < jf:  # whole: in place in the object
+                    data = host[base + j * cl: base + (j + 1) * cl]
+                    assert not (slots[j] != 0xAB).any(), (i, j)  # tail slot untouched
+                elif j == jf and part:
+                    data = np.zeros(cl, dtype=np.uint8)
+                    data[:part] = host[base + j * cl: base + j * cl + part]
+                    assert np.array_equal(slots[j, :cl], data) and not slots[j, cl:].any(), (i, j)
+                else:  # all zero
+                    data = np.zeros(cl, dtype=np.uint8)
+                    assert not (slots[j] != 0xAB).any(), (i, j)
+                if i % 13 == 0 or j == jf:
+                    assert m1[g + ns - 1, j].tobytes() == hashlib.md5(data.tobytes()).digest(), (i, j)
+            toff += k * cls
+        g += ns
+    arena.free()
