@@ -109,6 +109,39 @@ __device__ __forceinline__ void lookup_pair(int j0, bool two, const u32x4 d0, co
   }
 }
 
+// Split-nibble tables without bank conflicts (the A/B of DESIGN.md §4's LDS
+// floor; NXEC_EM_TABLES=nib, K = 10): source j's products of x and of x << 4
+// (x = 0..15, 4 rows packed per entry) in 32 copies, copy c at bank c, so a
+// 32-lane group's ds_read_b32 is served in one LDS cycle whatever the bytes.
+// Entry (j, x, half, c) at byte j*4096 + x*256 + half*128 + 4c: the address
+// of a nibble is one v_perm_b32 (nibble into byte 1, the lane's 4c | 128*half
+// into byte 0).  Two lookups per byte (~3.75 VALU per byte against the
+// single-copy table's 1.5, and 4x the table bytes: 40 KiB for k = 10).
+__device__ __forceinline__ void build_nib_tables(const uint8_t *coef, int k, int rows, uint32_t *tab) {
+  for (int i = threadIdx.x; i < k * 1024; i += blockDim.x) {
+    const int half = (i >> 5) & 1, nib = (i >> 6) & 15, j = i >> 10;
+    const uint32_t x = half ? static_cast<uint32_t>(nib) << 4 : static_cast<uint32_t>(nib);
+    uint32_t e = 0;
+    for (int r = 0; r < rows; r++) e |= dev::gf_mul_dev(coef[r * k + j], x) << (8 * r);
+    tab[i] = e;
+  }
+}
+__device__ __forceinline__ void lookup_nib(int j, const u32x4 d, uint32_t lane4, uint32_t acc[16]) {
+  const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+  const int t = j * 4096;
+  const uint32_t lane4h = lane4 | 128u;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t wl = w[q] & 0x0F0F0F0Fu, wh = (w[q] >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t sel = 0x0C0C0000u | ((4u + b) << 8);
+      const uint32_t al = __builtin_amdgcn_perm(wl, lane4, sel), ah = __builtin_amdgcn_perm(wh, lane4h, sel);
+      acc[4 * q + b] = __builtin_amdgcn_bitop3_b32(acc[4 * q + b], ent(t, al), ent(t, ah), 0x96);
+    }
+  }
+}
+
 // prefetch ring depth: as many 4K-VGPR source buffers as fit in ~200 VGPRs
 // (the rest of the code role needs ~20 with buffer-resource addressing)
 template <int K>
@@ -123,6 +156,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t em_rsrc(const void *base) {
 }
 __device__ __forceinline__ u32x4 em_load(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2));
+}
+__device__ __forceinline__ u32x4 em_load_cached(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 __device__ __forceinline__ void em_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)), v),
@@ -233,6 +269,65 @@ __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes
   }
 }
 
+// Hash lanes of the HG variant (NXEC_EM_HASHSRC=global):
+// a lane whose chunk is a source (gsrc != nullptr) reads its 256 bytes of
+// the step from global memory -- the code waves loaded them a few steps
+// earlier with caching loads, so they come from L2 / the Infinity Cache --
+// instead of an LDS row; output chunks keep their LDS rows.  Same
+// double-buffered timing as hash_rows.
+__device__ __forceinline__ void hash_rows_hg(const uint8_t *buf, uint32_t buf_bytes, int lds_row, const uint8_t *gsrc,
+                                             bool active, int nsteps, uint32_t (&st)[4]) {
+  const u32x4 *row = reinterpret_cast<const u32x4 *>(buf + lds_row * kEmRow);
+  md5_init(st);
+  auto fetch = [&](int step, uint32_t(&m)[kEncMd5Step / 4]) {
+    if (gsrc) {
+      const uint8_t *g = gsrc + static_cast<int64_t>(step) * kEncMd5Step;
+#pragma unroll
+      for (int i = 0; i < kEmVecs; i++) {
+        const u32x4 x = dev::ld_global(g + 16 * i);
+        m[4 * i] = x.x, m[4 * i + 1] = x.y, m[4 * i + 2] = x.z, m[4 * i + 3] = x.w;
+      }
+    } else {
+      const u32x4 *p = row + (step & 1) * (buf_bytes / 16);
+#pragma unroll
+      for (int i = 0; i < kEmVecs; i++) {
+        const u32x4 x = p[i];
+        m[4 * i] = x.x, m[4 * i + 1] = x.y, m[4 * i + 2] = x.z, m[4 * i + 3] = x.w;
+      }
+    }
+  };
+  auto hash = [&](const uint32_t(&m)[kEncMd5Step / 4]) {
+#pragma unroll
+    for (int b = 0; b < kEncMd5Step / 64; b++) md5_block(st, m + 16 * b);
+  };
+  uint32_t m0[kEncMd5Step / 4], m1[kEncMd5Step / 4];
+  lds_barrier();
+  if (active) fetch(0, m0);
+  int step = 1;
+  for (; step + 2 <= nsteps; step += 2) {
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+    }
+    lds_barrier();
+    if (active) {
+      fetch(step + 1, m0);
+      hash(m1);
+    }
+  }
+  if (step < nsteps) {
+    lds_barrier();
+    if (active) {
+      fetch(step, m1);
+      hash(m0);
+      hash(m1);
+    }
+  } else if (active) {
+    hash(m0);
+  }
+}
+
 // PROBE (design probes only, K = 10, NXEC_EM_PROBE; outputs are NOT valid):
 // bit 0 skips the MD5 rounds (hash lanes only read their rows), bit 1 skips
 // the table lookups (parity = first source), bit 2 skips every global load
@@ -241,16 +336,21 @@ __device__ __forceinline__ void hash_rows(const uint8_t *buf, uint32_t buf_bytes
 // template parameter, not a runtime flag: a wave-uniform branch around the
 // sources' LDS writes kept every ring buffer live longer and spilled from
 // k = 8 (180 instead of 256+ VGPRs at k = 10).
-template <int K, bool HSRC, int PROBE = 0>
+template <int K, bool HSRC, int PROBE = 0, bool NIB = false, bool HG = false>
 __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
-  const int nh = a.nhashed;  // hashed chunks per stripe: LDS rows per stripe
-  constexpr int hsrc = HSRC ? K : 0;  // rows before the outputs' rows
+  const int nh = a.nhashed;  // hashed chunks per stripe
+  // LDS rows per stripe: every hashed chunk, or (HG) only the outputs
+  const int nrow = HG ? a.p : nh;
+  constexpr int hsrc = HSRC && !HG ? K : 0;  // rows before the outputs' rows
   const int S = a.stripes_per_group;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
-  uint8_t *buf = lds + K * 1024;
-  const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
-  build_tables<1>(a.coef, K, a.p, tab);
+  uint8_t *buf = lds + K * (NIB ? 4096 : 1024);
+  const uint32_t buf_bytes = static_cast<uint32_t>(S * nrow * kEmRow);
+  if (NIB)
+    build_nib_tables(a.coef, K, a.p, tab);
+  else
+    build_tables<1>(a.coef, K, a.p, tab);
   __syncthreads();
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * S;
   const int nS = static_cast<int>(min(static_cast<int64_t>(S), a.nstripes - s0));
@@ -281,13 +381,15 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
     const __amdgpu_buffer_rsrc_t rsrc_dst = em_rsrc(a.dst + s0 * a.dst_stripe_stride);
     const uint32_t vsrc = static_cast<uint32_t>(ls * a.src_stripe_stride) + v * 16;
     const uint32_t vdst = static_cast<uint32_t>(ls * a.dst_stripe_stride) + v * 16;
-    uint8_t *row = buf + ls * nh * kEmRow + v * 16;
+    uint8_t *row = buf + ls * nrow * kEmRow + v * 16;
     auto load = [&](int step, u32x4(&d)[K]) {
       const uint32_t off = static_cast<uint32_t>(step) * kEncMd5Step;
 #pragma unroll
       for (int j = 0; j < K; j++) {
         if (PROBE & 4)  // no HBM traffic: a value the compiler cannot fold
           d[j] = u32x4{vsrc ^ off, off + j, vsrc, static_cast<uint32_t>(j)};
+        else if (HG)  // the hash lanes read these bytes again a few steps later
+          d[j] = em_load_cached(rsrc_src, vsrc, a.src_off[j] + off);
         else
           d[j] = em_load(rsrc_src, vsrc, a.src_off[j] + off);
       }
@@ -311,7 +413,13 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
         if (PROBE & 2) {
           if (j == 0) acc[0] = d[0].x, acc[5] = d[0].y, acc[10] = d[0].z, acc[15] = d[0].w;
         } else if (a.p > 0) {  // wave-uniform (p = 0: a verified copy, no rows to compute)
-          lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+          if (NIB) {
+            const uint32_t lane4 = (threadIdx.x & 31u) * 4u;
+            lookup_nib(j, d[j], lane4, acc);
+            if (j + 1 < K) lookup_nib(j + 1, d[j + 1], lane4, acc);
+          } else {
+            lookup_pair(j, j + 1 < K, d[j], d[j + 1 < K ? j + 1 : j], acc);
+          }
         }
         // materialise the accumulators per source pair: left alone, LLVM
         // turns the XOR chains into trees over all k sources, which keeps 16
@@ -369,7 +477,14 @@ __global__ __launch_bounds__(kEmBlock) void k_mul_md5(const MulMd5Args a) {
   const int h = threadIdx.x - kEmCodeLanes;
   const bool active = h < nS * nh;
   uint32_t st[4];
-  hash_rows<PROBE>(buf, buf_bytes, h, active, nsteps, st);
+  if (HG) {
+    const int hls = active ? h / nh : 0, hc = active ? h - hls * nh : 0;
+    const bool gsrc = active && hc < K;
+    const uint8_t *gp = gsrc ? a.src + (s0 + hls) * a.src_stripe_stride + a.src_off[hc] : nullptr;
+    hash_rows_hg(buf, buf_bytes, gsrc ? 0 : hls * nrow + (hc - K), gp, active, nsteps, st);
+  } else {
+    hash_rows<PROBE>(buf, buf_bytes, h, active, nsteps, st);
+  }
   if (active) {
     md5_pad_aligned(st, static_cast<uint64_t>(a.len));
     const int ls = h / nh, c = h - ls * nh;
@@ -997,6 +1112,8 @@ constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int
 const std::array<EmKernel, kEncMd5MaxK> kEm[2] = {em_table<false>(std::make_integer_sequence<int, kEncMd5MaxK>{}),
                                                   em_table<true>(std::make_integer_sequence<int, kEncMd5MaxK>{})};
 
+const EmKernel kEmNib = &k_mul_md5<10, true, 0, true>;
+const EmKernel kEmHg = &k_mul_md5<10, true, 0, false, true>;
 const EmKernel kEmProbe[8] = {&k_mul_md5<10, true, 0>, &k_mul_md5<10, true, 1>, &k_mul_md5<10, true, 2>,
                               &k_mul_md5<10, true, 3>, &k_mul_md5<10, true, 4>, &k_mul_md5<10, true, 5>,
                               &k_mul_md5<10, true, 6>, &k_mul_md5<10, true, 7>};
@@ -1050,6 +1167,16 @@ int prepare_encode_md5() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_gather_md5): %s", hipGetErrorString(e));
   }
+  for (FmKernel fn : kFmProbe) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5 probe): %s", hipGetErrorString(e));
+  }
+  {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEmNib), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 nib): %s", hipGetErrorString(e));
+    e = hipFuncSetAttribute(reinterpret_cast<const void *>(kEmHg), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
+    if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 hg): %s", hipGetErrorString(e));
+  }
   for (EmKernel fn : kEmProbe) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 probe): %s", hipGetErrorString(e));
@@ -1076,10 +1203,23 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   if (const char *e = std::getenv("NXEC_EM_PRIO")) a.hash_prio = std::atoi(e);
   const int64_t grid = (a.nstripes + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
-  const int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
+  int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
   if (const char *e = std::getenv("NXEC_EM_PROBE"))
     if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 7];
+  // A/B: conflict-free split-nibble tables (k = 10, sources hashed; 40 KiB of tables)
+  if (const char *e = std::getenv("NXEC_EM_TABLES"))
+    if (e[0] == 'n' && a.k == 10 && a.hash_src && 10 * 4096 + 2 * S * n * kEmRow <= kEmLds) {
+      fn = kEmNib;
+      lds = 10 * 4096 + static_cast<int>(2 * S * n * kEmRow);
+    }
+  // A/B: hash lanes read the source chunks from global memory (only the
+  // outputs' rows in LDS; k = 10, sources hashed, full-output copies off)
+  if (const char *e = std::getenv("NXEC_EM_HASHSRC"))
+    if (e[0] == 'g' && a.k == 10 && a.hash_src && a.hash_dst && !a.any_copy && !a.ok) {
+      fn = kEmHg;
+      lds = 10 * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
+    }
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();

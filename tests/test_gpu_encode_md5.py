@@ -355,3 +355,29 @@ def test_decode_object_verify_many_losses(gpu_ctx):
     assert np.array_equal(out.download()[:nf * k * M], obj[:nf * k * M])
     for b in (ob, par, tail, md5, cb, out, ok, nb):
         b.free()
+
+
+@pytest.mark.parametrize("env", [("NXEC_EM_TABLES", "nib"), ("NXEC_EM_HASHSRC", "global")])
+@pytest.mark.parametrize("M,nstripes", [(256, 1), (4096, 37), (65536, 300)])
+def test_fused_encode_md5_variants_ab(gpu_ctx, monkeypatch, env, M, nstripes):
+    """The fused write kernel's A/B variants (k = 10): conflict-free
+    split-nibble tables (NXEC_EM_TABLES=nib) and hash lanes reading the source
+    chunks from global memory (NXEC_EM_HASHSRC=global).  Parity and digests equal
+    the default kernel's and the oracle / hashlib."""
+    n, k = 14, 10
+    length = nstripes * k * M
+    obj = fill_bytes(length, 7300 + M)
+    ob = nxec.DeviceBuffer(length)
+    ob.upload(obj)
+    par, dig = _encode_object(gpu_ctx, n, k, M, ob, length, fused=True)
+    monkeypatch.setenv(*env)
+    par2, dig2 = _encode_object(gpu_ctx, n, k, M, ob, length, fused=True)
+    ob.free()
+    assert np.array_equal(par, par2)
+    assert np.array_equal(dig, dig2)
+    for s in sorted({0, nstripes - 1}):
+        st = oracle.rs_encode(n, k, obj[s * k * M:(s + 1) * k * M], M)
+        for i in range(n - k):
+            assert np.array_equal(par2[s, i], st[k + i]), (s, i)
+        for c in range(n):
+            assert dig2[s, c].tobytes().hex() == hashlib.md5(st[c].tobytes()).hexdigest(), (s, c)
