@@ -742,6 +742,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     rq[i] = v;
   }
   __syncthreads();
+  if (a.wg_clock && threadIdx.x == 0) a.wg_clock[blockIdx.x * 3] = __builtin_amdgcn_s_memrealtime();
   const int nsteps = a.wg_steps[blockIdx.x];
   auto steps_of = [](int64_t len) { return static_cast<int>((len + kEncMd5Step - 1) / kEncMd5Step); };
 
@@ -981,6 +982,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         run(step + j, ring[j]);
       }
     }
+    if (a.wg_clock && threadIdx.x == 0) a.wg_clock[blockIdx.x * 3 + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
 
@@ -1083,6 +1085,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   } else {
     proc(m0);
   }
+  if (a.wg_clock && threadIdx.x == kEmCodeLanes) a.wg_clock[blockIdx.x * 3 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
 using FmKernel = void (*)(const FilesMd5Args);

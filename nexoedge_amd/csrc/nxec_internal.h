@@ -273,6 +273,9 @@ struct FilesMd5Args {
   // partial one (zero-padded) is written to the tail arena; the whole ones
   // stay where they are in the object, the all-zero ones are not written
   int32_t tail_partial_only;
+  // NXEC_FILES_CLOCK=1 (diagnostics): per workgroup, s_memrealtime at the
+  // start, at the end of code wave 0 and at the end of hash wave 0
+  unsigned long long *wg_clock;
 };
 // Slot plan for `lens` (descending): fills slot_first / slot_reqs / wg_steps
 // and the args' nslots / slots_per_group / max_list.  NXEC_FILES_PACK=0 gives

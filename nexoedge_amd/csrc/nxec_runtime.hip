@@ -1206,9 +1206,39 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
     fa.p = p;
     fa.tail_partial_only = (flags & NXEC_OBJECTS_TAIL_INPLACE) && tail_direct ? 1 : 0;
     std::memcpy(fa.coef, prow, size_t(p) * k);
+    // NXEC_FILES_CLOCK=1: per-workgroup timestamps (diagnostics, stderr)
+    static const bool wg_clock = [] {
+      const char *e = std::getenv("NXEC_FILES_CLOCK");
+      return e && e[0] == '1';
+    }();
+    const int64_t nwg = static_cast<int64_t>(wg_steps.size());
+    unsigned long long *d_clock = nullptr;
+    if (wg_clock && !rc && hipMalloc(&d_clock, size_t(nwg) * 3 * 8) == hipSuccess) {
+      (void)hipMemsetAsync(d_clock, 0, size_t(nwg) * 3 * 8, st);
+      fa.wg_clock = d_clock;
+    }
     if (!rc) rc = launch_files_md5(fa, ctx->num_cus, st);
     const double t_launch = timing ? ms_since(th0) : 0;
     const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
+    if (d_clock) {  // per workgroup: start, code end, hash end (100 MHz), by slot composition
+      std::vector<unsigned long long> c(size_t(nwg) * 3);
+      if (hipMemcpy(c.data(), d_clock, c.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+        unsigned long long t0 = ~0ull;
+        for (int64_t b = 0; b < nwg; b++) t0 = std::min(t0, c[size_t(b) * 3]);
+        const int64_t S = fa.slots_per_group;
+        for (int64_t b = 0; b < nwg; b++) {
+          int nfull = 0, ntail = 0;
+          for (int64_t g = b * S; g < std::min<int64_t>((b + 1) * S, fa.nslots); g++)
+            for (int32_t i = slot_first[size_t(g)]; i < slot_first[size_t(g) + 1]; i++)
+              (f_tsrc[size_t(slot_reqs[size_t(i)])] ? ntail : nfull)++;
+          std::fprintf(stderr, "wg %lld steps %d full %d tail %d start %.1f code_end %.1f hash_end %.1f us\n",
+                       static_cast<long long>(b), wg_steps[size_t(b)], nfull, ntail,
+                       (c[size_t(b) * 3] - t0) * 0.01, (c[size_t(b) * 3 + 1] - t0) * 0.01,
+                       (c[size_t(b) * 3 + 2] - t0) * 0.01);
+        }
+      }
+      (void)hipFree(d_clock);
+    }
     if (timing)
       std::fprintf(stderr, "nxec_encode_objects: %d objects, %zu requests: plan %.3f ms, tables + launch %.3f ms, "
                    "wait %.3f ms\n", nobjects, f_len.size(), t_plan, t_launch - t_plan, ms_since(th0) - t_launch);
