@@ -773,8 +773,15 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // tail bytes [j*cl, (j+1)*cl), valid below min((j+1)*cl, rem): `tl` = cl
     // (0 for a full stripe), `jf` = chunks wholly valid, `last` = the valid
     // bytes of chunk jf (32-bit: cl <= 1 GiB), `end` = the end of the tail's
-    // last 16-byte line (nothing at or past it is read)
-    auto tail_state = [&](int li, int64_t cl, uint32_t &tl, uint32_t &jf, uint32_t &last, const uint8_t *&end) {
+    // last 16-byte line (nothing at or past it is read), `zf` = the first
+    // all-zero chunk (read from the zero scratch line, never masked), `jc` =
+    // the first chunk whose 16-byte column vectors can run past `end` (only
+    // chunks jc..zf-1 are clamped when loaded and, in place, shifted / masked
+    // when computed: below jc a vector past the chunk's own end reads the next
+    // chunk's bytes, which only reach parity bytes past cl -- outside the
+    // parity chunk -- and row bytes the hash lanes mask off)
+    auto tail_state = [&](int li, int64_t cl, uint32_t &tl, uint32_t &jf, uint32_t &last, const uint8_t *&end,
+                          uint32_t &jc, uint32_t &zf) {
       const uint64_t tb = act ? q[li * rec + K + a.p + 2] : uint64_t(0);
       const int64_t rem = act ? static_cast<int64_t>(q[li * rec + K + a.p + 3]) : int64_t(0);
       const int64_t f = tb && cl > 0 ? min(rem / cl, static_cast<int64_t>(K)) : 0;
@@ -782,6 +789,10 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       jf = static_cast<uint32_t>(f);
       last = f < K && tb ? static_cast<uint32_t>(rem - f * cl) : 0u;
       end = reinterpret_cast<const uint8_t *>((tb + static_cast<uint64_t>(rem) + 15) & ~uint64_t(15));
+      const int64_t cls = (cl + 15) / 16 * 16;
+      zf = tb ? static_cast<uint32_t>(f < K ? f + (last ? 1 : 0) : K) : static_cast<uint32_t>(K);
+      jc = tb ? static_cast<uint32_t>(rem >= cls && cl > 0 ? min((rem - cls) / cl + 1, static_cast<int64_t>(K)) : 0)
+              : static_cast<uint32_t>(K);
     };
     auto valid_of = [](int j, uint32_t tl, uint32_t jf, uint32_t last) {
       return static_cast<int32_t>(static_cast<uint32_t>(j) < jf ? tl : static_cast<uint32_t>(j) == jf ? last : 0u);
@@ -800,9 +811,9 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
                            : a.scratch + v * 16;
     };
     set_src(0, tmax_of(len0) >= 0);
-    uint32_t ltl, ljf, llast;
+    uint32_t ltl, ljf, llast, ljc, lzf;
     const uint8_t *lend;
-    tail_state(0, len0, ltl, ljf, llast, lend);
+    tail_state(0, len0, ltl, ljf, llast, lend, ljc, lzf);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
       const bool wtl = __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
@@ -814,10 +825,14 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         // first byte (the compute step shifts it into place), or the scratch
         // line once nothing of the tail is left
         const uint8_t *pj = sp[j] + off;
-        if (wtl && ltl)
-          pj = pj + 16 <= lend ? pj
-               : pj < lend     ? reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pj) & ~uintptr_t(15))
-                               : a.scratch + v * 16;
+        if (wtl && ltl && static_cast<uint32_t>(j) >= ljc) {  // the few chunks that reach the tail's end
+          if (static_cast<uint32_t>(j) >= lzf)
+            pj = a.scratch + v * 16;  // all zero
+          else
+            pj = pj + 16 <= lend ? pj
+                 : pj < lend     ? reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pj) & ~uintptr_t(15))
+                                 : a.scratch + v * 16;
+        }
         // plain (cached) loads: a chunk that is not 128-byte aligned (an
         // object at any 16-byte offset, a tail at any byte) shares its
         // boundary lines between consecutive steps; streaming loads fetched
@@ -838,7 +853,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           lT = steps_of(ln);
           ltcl = max(tmax_of(ln), 0);
           set_src(lr, tmax_of(ln) >= 0);
-          tail_state(lr, ln, ltl, ljf, llast, lend);
+          tail_state(lr, ln, ltl, ljf, llast, lend, ljc, lzf);
         } else {
           lt = lT - 1;  // past the slot's end: re-read the last step
         }
@@ -847,7 +862,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // compute cursor
     int cr = 0, ct = 0, cT = lT, ctmax = act ? tmax_of(len0) : -1;
     bool live = act;
-    uint32_t ctl = ltl, cjf = ljf, clast = llast;
+    uint32_t ctl = ltl, cjf = ljf, clast = llast, cjc = ljc, czf = lzf;
     const uint8_t *cend = lend;
     // the tail source and the tail arena's chunk 0 (chunk j at + j*cls), kept
     // in registers: no per-step read of the request table
@@ -912,8 +927,13 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         u32x4 x0 = d[j], x1 = d[j1];
         if (wtc && tl) {
           const int32_t nv0 = valid_of(j, ctl, cjf, clast) - pos, nv1 = valid_of(j1, ctl, cjf, clast) - pos;
-          if (nv0 < 16) x0 = tail_end(j, x0, nv0);
-          if (nv1 < 16) x1 = tail_end(j1, x1, nv1);
+          // shift / mask only where it matters: chunks jc..zf-1 (zero chunks
+          // were read as zeros); in copy mode also every chunk's last vector,
+          // whose bytes past cl go to the tail arena and must be zero
+          const bool m0 = static_cast<uint32_t>(j) < czf && (static_cast<uint32_t>(j) >= cjc || !a.tail_partial_only);
+          const bool m1 = static_cast<uint32_t>(j1) < czf && (static_cast<uint32_t>(j1) >= cjc || !a.tail_partial_only);
+          if (nv0 < 16 && m0) x0 = tail_end(j, x0, nv0);
+          if (nv1 < 16 && m1) x1 = tail_end(j1, x1, nv1);
           if (ok) {  // the zero-padded data chunks into the tail arena (in place: only the partial one)
             const bool part0 = j == static_cast<int>(cjf) && clast != 0, part1 = j1 == static_cast<int>(cjf) && clast != 0;
             if (!(PROBE & 4) && (!a.tail_partial_only || part0)) dev::st_global_stream(ctd + j * cls + pos, x0);
@@ -953,7 +973,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           cT = steps_of(ln);
           ctmax = tmax_of(ln);
           set_dst(cr);
-          tail_state(cr, ln, ctl, cjf, clast, cend);
+          tail_state(cr, ln, ctl, cjf, clast, cend, cjc, czf);
           ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
           ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
         } else {
