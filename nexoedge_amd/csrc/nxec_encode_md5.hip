@@ -704,7 +704,8 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 // last in-bounds vector, stores to scratch and leaves its LDS row alone.
 // PROBE (design probes only, K = 10, NXEC_FM_PROBE; outputs are NOT valid),
 // as k_mul_md5's: bit 0 no MD5 rounds, bit 1 no table lookups, bit 2 no
-// global loads or stores.
+// global loads or stores, bit 3 (alone, 8) no tail-arena stores, bit 4
+// (alone, 16) last stripes coded like whole stripes (no tail handling).
 template <int K, int PROBE = 0>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
@@ -816,7 +817,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     tail_state(0, len0, ltl, ljf, llast, lend, ljc, lzf);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
-      const bool wtl = __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
+      const bool wtl = !(PROBE & 16) && __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
 #pragma unroll
       for (int j = 0; j < K; j++) {
         // a tail chunk's 16 bytes are read where they lie (global loads take
@@ -907,7 +908,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
       const bool tl = live && ctl != 0;
-      const bool wtc = __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
+      const bool wtc = !(PROBE & 16) && __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
       if (wtc) {
         // wait for this step's loads here, in uniform control flow: a first
         // use inside the per-lane tail branches below would be counted
@@ -936,8 +937,8 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           if (nv1 < 16 && m1) x1 = tail_end(j1, x1, nv1);
           if (ok) {  // the zero-padded data chunks into the tail arena (in place: only the partial one)
             const bool part0 = j == static_cast<int>(cjf) && clast != 0, part1 = j1 == static_cast<int>(cjf) && clast != 0;
-            if (!(PROBE & 4) && (!a.tail_partial_only || part0)) dev::st_global_stream(ctd + j * cls + pos, x0);
-            if (!(PROBE & 4) && j + 1 < K && (!a.tail_partial_only || part1))
+            if (!(PROBE & 12) && (!a.tail_partial_only || part0)) dev::st_global_stream(ctd + j * cls + pos, x0);
+            if (!(PROBE & 12) && j + 1 < K && (!a.tail_partial_only || part1))
               dev::st_global_stream(ctd + j1 * cls + pos, x1);
           }
         }
@@ -1114,6 +1115,11 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int
   return {{&k_files_md5<Ks + 1>...}};
 }
 const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+// bit 3 alone: no tail-arena stores (everything else as the product);
+// bit 4 alone: last stripes read straight from the object like whole
+// stripes, no clamps, masks or tail stores (timing only)
+const FmKernel kFmProbe8 = &k_files_md5<10, 8>;
+const FmKernel kFmProbe16 = &k_files_md5<10, 16>;
 const FmKernel kFmProbe[8] = {&k_files_md5<10, 0>, &k_files_md5<10, 1>, &k_files_md5<10, 2>, &k_files_md5<10, 3>,
                               &k_files_md5<10, 4>, &k_files_md5<10, 5>, &k_files_md5<10, 6>, &k_files_md5<10, 7>};
 
@@ -1190,7 +1196,8 @@ int prepare_encode_md5() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_gather_md5): %s", hipGetErrorString(e));
   }
-  for (FmKernel fn : kFmProbe) {
+  for (FmKernel fn : {kFmProbe[0], kFmProbe[1], kFmProbe[2], kFmProbe[3], kFmProbe[4], kFmProbe[5], kFmProbe[6],
+                      kFmProbe[7], kFmProbe8, kFmProbe16}) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5 probe): %s", hipGetErrorString(e));
   }
@@ -1356,7 +1363,8 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
   FmKernel fn = kFm[a.k - 1];
   if (const char *e = std::getenv("NXEC_FM_PROBE"))
-    if (a.k == 10) fn = kFmProbe[std::atoi(e) & 7];
+    if (a.k == 10)
+      fn = std::atoi(e) == 8 ? kFmProbe8 : std::atoi(e) == 16 ? kFmProbe16 : kFmProbe[std::atoi(e) & 7];
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();

@@ -1042,6 +1042,8 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   const bool fused = want_fused && full_aligned;
   const bool sep = !fused;
   const bool need_pads = sep || !tail_direct;
+  // NXEC_OBJECTS_TAIL_INPLACE on the one-launch path (NXEC_FILES_TAIL=0 keeps the whole-tail pad copy)
+  const bool inplace = (flags & NXEC_OBJECTS_TAIL_INPLACE) && fused && tail_direct;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
@@ -1089,7 +1091,37 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
           for (int j = 0; j < k; j++) ritems.push_back({td + j * cls, cl, dig + j * 16});
           for (int i = 0; i < p; i++) ritems.push_back({par + i * M, cl, dig + (k + i) * 16});
         }
-        if (fused) {  // read from the object; the kernel writes the padded chunks to td
+        if (fused && inplace) {
+          // In place: the last stripe becomes an ordinary request.  Its data
+          // chunks below j0 are read where they lie in the object (no byte of
+          // theirs is zero padding, and their 16-byte column vectors stay
+          // inside the tail's last 16-byte line); chunks j0.. -- the partial
+          // one, the all-zero ones, and a whole one whose last vector would
+          // run past that line -- are first written zero-padded to their
+          // tail-arena slots by one small copy launch and read from there.
+          // The kernel then needs none of its per-step last-stripe handling
+          // (4.6 -> ~3.7 us per step of a last-stripe workgroup).
+          const uint8_t *tb = obj + nf * k * M;
+          const int64_t rem = lengths[o] - nf * k * M;
+          const int64_t jf = std::min<int64_t>(rem / cl, k), last = jf < k ? rem - jf * cl : 0;  // r % cl
+          const int64_t safe = static_cast<int64_t>(((reinterpret_cast<uintptr_t>(tb) + rem + 15) & ~uintptr_t(15)) -
+                                                    reinterpret_cast<uintptr_t>(tb));
+          (void)last;
+          int64_t j0 = jf;  // the partial chunk (last > 0), else the first all-zero one (or k: none)
+          const int64_t jov = safe >= cls ? (safe - cls) / cl + 1 : 0;  // first chunk reading past `safe`
+          j0 = std::min(j0, jov);
+          for (int j = 0; j < k; j++) q_src.push_back(j < j0 ? tb + j * cl : td + j * cls);
+          if (j0 < k) {
+            pads.push_back({tb + j0 * cl, td + j0 * cls, rem - j0 * cl, cl, cls, k - j0});
+            pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
+            pad_blocks += (cls / 16 * (k - j0) + 256 * kPadVecs - 1) / (256 * kPadVecs);
+          }
+          for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
+          q_len.push_back(cl);
+          q_dig.push_back(dig);
+          q_tsrc.push_back(nullptr);
+          q_trem.push_back(0);
+        } else if (fused) {  // read from the object; the kernel writes the padded chunks to td
           for (int j = 0; j < k; j++) q_src.push_back(td + j * cls);
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(cl);
@@ -1188,8 +1220,10 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   const int T0 = 10;  // the first ten tables belong to the fused launch
   auto dptr = [&](int i) { return slot->d + off[i + T0]; };
   if (fused) {
-    // no pad copy: last stripes read their object and write the tail arena themselves
-    if (!rc && !tail_direct)
+    // the whole-tail pad copy (NXEC_FILES_TAIL=0) or, in place, the few chunks
+    // of each last stripe that are not read from the object; otherwise last
+    // stripes read their object and the kernel writes the tail arena itself
+    if (!rc && !pads.empty())
       rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
                              int64_t(pads.size()), pad_blocks, st);
     fa.tail_src = reinterpret_cast<const uint8_t *const *>(slot->d + off[8]);
@@ -1204,7 +1238,7 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
     fa.wg_steps = reinterpret_cast<const int32_t *>(slot->d + off[7]);
     fa.k = k;
     fa.p = p;
-    fa.tail_partial_only = (flags & NXEC_OBJECTS_TAIL_INPLACE) && tail_direct ? 1 : 0;
+    fa.tail_partial_only = 0;  // in place, last stripes reach the kernel as ordinary requests
     std::memcpy(fa.coef, prow, size_t(p) * k);
     // NXEC_FILES_CLOCK=1: per-workgroup timestamps (diagnostics, stderr)
     static const bool wg_clock = [] {

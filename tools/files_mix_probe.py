@@ -6,6 +6,8 @@ spends its steps.  Several 4096-file batches, each timed in one process:
   even5     every file 5 MiB: one last stripe each, 512 KiB chunks, all whole
   ragged    every file's length uniform in [1 B, 10 MiB): one ragged last stripe each
   mix       bench.py's batch: uniform in [1 B, 20 MiB] (full + ragged)
+  al16/al8  last stripes of whole chunks only, chunk starts 16-byte aligned /
+            all 8 bytes off (the cost of misaligned loads)
 
 each with the tail arena written whole (default) and with
 NXEC_OBJECTS_TAIL_INPLACE (only each last stripe's partial data chunk);
@@ -87,6 +89,10 @@ sets = {
     "even5": [k * M // 2] * 4096,
     "ragged": [int(x) for x in rng.integers(1, k * M, size=4096)],
     "mix": [int(x) for x in np.random.default_rng(1234).integers(1, 2 * k * M + 1, size=4096)],
+    # whole last-stripe chunks only (length = k * cl), chunk starts 16-byte
+    # aligned (cl % 16 == 0) or all misaligned by 8: the cost of misaligned loads
+    "al16": [k * 16 * int(x) for x in np.random.default_rng(99).integers(1, M // 16, size=4096)],
+    "al8": [k * (16 * int(x) + 8) for x in np.random.default_rng(99).integers(1, M // 16, size=4096)],
 }
 which = sys.argv[1:] or list(sets)
 for name in which:

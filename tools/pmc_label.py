@@ -12,10 +12,15 @@ import subprocess
 import sys
 
 fdir, wdir, sub, cmd = sys.argv[1:5]
-labels = [(a.rsplit(":", 1)[0], int(a.rsplit(":", 1)[1])) for a in sys.argv[5:]]
+labels = [(a.rsplit(":", 1)[0], a.rsplit(":", 1)[1]) for a in sys.argv[5:]]
 out = subprocess.run([sys.executable, __file__.replace("pmc_label.py", "pmc_dispatch.py"), fdir, wdir, sub],
                      capture_output=True, text=True, check=True).stdout
 rows = [json.loads(l) for l in out.splitlines() if l.strip()]
+# one LABEL:BYTES* pair labels every dispatch the same (workloads whose every
+# launch of the kernel moves the same bytes)
+if len(labels) == 1 and labels[0][1].endswith("*"):
+    labels = labels * len(rows)
+labels = [(lab, int(b.rstrip("*"))) for lab, b in labels]
 if len(labels) != len(rows):
     sys.exit(f"{len(rows)} dispatches, {len(labels)} labels")
 disp = []
