@@ -42,6 +42,10 @@ extern "C" {
 const char *nxec_last_error(void);
 /* library version string */
 const char *nxec_version(void);
+/* 1 when the library was built with the design-probe kernels (make PROBES=1:
+ * the NXEC_EM_PROBE / NXEC_EM_TABLES / NXEC_EM_HASHSRC / NXEC_FM_PROBE A/B
+ * variants of DESIGN.md section 4), 0 for the product build */
+int nxec_design_probes(void);
 
 /* ---------------------------------------------------------------------------
  * 1. Host GF(2^8) math (poly 0x11d) -- replaces the ISA-L calls in rs.cc.

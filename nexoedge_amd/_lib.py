@@ -28,6 +28,7 @@ i64 = C.c_int64
 _PROTOS = {
     "nxec_last_error": (C.c_char_p, []),
     "nxec_version": (C.c_char_p, []),
+    "nxec_design_probes": (C.c_int, []),
     "nxec_gf_mul": (C.c_ubyte, [C.c_ubyte, C.c_ubyte]),
     "nxec_gf_inv": (C.c_ubyte, [C.c_ubyte]),
     "nxec_gf_gen_rs_matrix": (None, [vp, C.c_int, C.c_int]),

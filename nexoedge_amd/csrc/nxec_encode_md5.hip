@@ -46,6 +46,15 @@
 #include "nxec_device.h"
 #include "nxec_internal.h"
 
+// Design-probe kernels (role probes and the LDS-table A/B variants, selected
+// by environment variables) are built only with `make PROBES=1`: they are
+// measurement tools, not product paths, and double this file's build time.
+#ifndef NXEC_DESIGN_PROBES
+#define NXEC_DESIGN_PROBES 0
+#endif
+
+extern "C" int nxec_design_probes(void) { return NXEC_DESIGN_PROBES; }
+
 namespace nxec {
 
 namespace {
@@ -1115,6 +1124,7 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int
   return {{&k_files_md5<Ks + 1>...}};
 }
 const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+#if NXEC_DESIGN_PROBES
 // bit 3 alone: no tail-arena stores (everything else as the product);
 // bit 4 alone: last stripes read straight from the object like whole
 // stripes, no clamps, masks or tail stores (timing only)
@@ -1122,6 +1132,7 @@ const FmKernel kFmProbe8 = &k_files_md5<10, 8>;
 const FmKernel kFmProbe16 = &k_files_md5<10, 16>;
 const FmKernel kFmProbe[8] = {&k_files_md5<10, 0>, &k_files_md5<10, 1>, &k_files_md5<10, 2>, &k_files_md5<10, 3>,
                               &k_files_md5<10, 4>, &k_files_md5<10, 5>, &k_files_md5<10, 6>, &k_files_md5<10, 7>};
+#endif
 
 using GmKernel = void (*)(const GatherMd5Args);
 template <bool HSRC, int... Ks>
@@ -1141,11 +1152,13 @@ constexpr std::array<EmKernel, sizeof...(Ks)> em_table(std::integer_sequence<int
 const std::array<EmKernel, kEncMd5MaxK> kEm[2] = {em_table<false>(std::make_integer_sequence<int, kEncMd5MaxK>{}),
                                                   em_table<true>(std::make_integer_sequence<int, kEncMd5MaxK>{})};
 
+#if NXEC_DESIGN_PROBES
 const EmKernel kEmNib = &k_mul_md5<10, true, 0, true>;
 const EmKernel kEmHg = &k_mul_md5<10, true, 0, false, true>;
 const EmKernel kEmProbe[8] = {&k_mul_md5<10, true, 0>, &k_mul_md5<10, true, 1>, &k_mul_md5<10, true, 2>,
                               &k_mul_md5<10, true, 3>, &k_mul_md5<10, true, 4>, &k_mul_md5<10, true, 5>,
                               &k_mul_md5<10, true, 6>, &k_mul_md5<10, true, 7>};
+#endif
 
 }  // namespace
 
@@ -1196,6 +1209,7 @@ int prepare_encode_md5() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_gather_md5): %s", hipGetErrorString(e));
   }
+#if NXEC_DESIGN_PROBES
   for (FmKernel fn : {kFmProbe[0], kFmProbe[1], kFmProbe[2], kFmProbe[3], kFmProbe[4], kFmProbe[5], kFmProbe[6],
                       kFmProbe[7], kFmProbe8, kFmProbe16}) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
@@ -1211,6 +1225,7 @@ int prepare_encode_md5() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5 probe): %s", hipGetErrorString(e));
   }
+#endif
   return NXEC_OK;
 }
 
@@ -1235,6 +1250,7 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
   int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
+#if NXEC_DESIGN_PROBES
   if (const char *e = std::getenv("NXEC_EM_PROBE"))
     if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 7];
   // A/B: conflict-free split-nibble tables (k = 10, sources hashed; 40 KiB of tables)
@@ -1250,6 +1266,7 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
       fn = kEmHg;
       lds = 10 * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
     }
+#endif
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();
@@ -1362,9 +1379,11 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
   const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
   FmKernel fn = kFm[a.k - 1];
+#if NXEC_DESIGN_PROBES
   if (const char *e = std::getenv("NXEC_FM_PROBE"))
     if (a.k == 10)
       fn = std::atoi(e) == 8 ? kFmProbe8 : std::atoi(e) == 16 ? kFmProbe16 : kFmProbe[std::atoi(e) & 7];
+#endif
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);
   hipError_t e = hipGetLastError();

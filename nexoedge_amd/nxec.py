@@ -201,6 +201,11 @@ def proxy_repair_using_car(path: str) -> bool:
     return bool(car.value)
 
 
+def design_probes() -> bool:
+    """True when libnxec carries the design-probe kernels (make PROBES=1)."""
+    return bool(lib.nxec_design_probes())
+
+
 def device_count() -> int:
     c = C.c_int(0)
     rc = lib.nxec_device_count(C.byref(c))

@@ -15,6 +15,8 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from nexoedge_amd import nxec  # noqa: E402
 
+if not nxec.design_probes():
+    sys.exit("libnxec was built without the design-probe kernels: make clean && make PROBES=1")
 n, k, M = 14, 10, 1 << 20
 p = n - k
 ctx = nxec.Context(0)
