@@ -206,17 +206,15 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    ("rs10_4", 1 << 20, "auto"): ("r03_pmc_rs10_4.json", ("encode", "recover")),
-    ("rs10_4", 1 << 20, "natural"): ("r03_pmc_rs10_4.json", ("encode", "recover")),
-    ("rs10_4", 1 << 20, "recover"): ("r02_pmc_rs10_4_layout_recover.json", ("encode", "recover")),
-    ("mixed16", 4 << 20, "auto"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
-    ("mixed16", 4 << 20, "recover"): ("r02_pmc_mixed16_4m_layout.json", "encode"),
-    ("mixed16", 4 << 20, "natural"): ("r02_pmc_mixed16_4m_packed.json", "encode"),
-    ("write14", 1 << 20, "auto"): ("r02_pmc_write14_fused.json", "encode_md5_fused"),
-    ("write14", 1 << 20, "natural"): ("r02_pmc_write14_fused.json", "encode_md5_fused"),
-    ("repair12", 1 << 20, "natural"): ("r02_pmc_repair12.json", "repair_fused_perm12"),
-    ("repair12", 1 << 20, "auto"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
-    ("repair12", 1 << 20, "recover"): ("r02_pmc_repair12_layout.json", "repair_fused_perm12"),
+    # round-4 passes on the shipped library (tools/gpu_r04_final.sh; every dispatch
+    # of the roofline kernel labelled with the bench line's bytes per launch);
+    # tests/test_bench_line.py checks each file's lib_sha16 against libnxec.so;
+    # only the default layout the passes ran with (other layouts report traffic null)
+    ("rs10_4", 1 << 20, "auto"): ("r04_pmc_rs10_4.json", "encode_recover"),
+    ("mixed16", 4 << 20, "auto"): ("r04_pmc_mixed16.json", "encode_recover"),
+    ("write14", 1 << 20, "auto"): ("r04_pmc_write14.json", "encode_md5_fused"),
+    ("repair12", 1 << 20, "auto"): ("r04_pmc_repair12.json", "repair_fused_perm12"),
+    ("files", 1 << 20, "auto"): ("r04_pmc_files.json", "encode_objects_md5"),
 }
 
 

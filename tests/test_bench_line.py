@@ -58,6 +58,21 @@ def test_traffic_carries_its_source(monkeypatch):
     assert bench.load_traffic(A, "rs10_4", 1) == (None, None)
 
 
+def test_pmc_summaries_measured_this_library():
+    """Every PMC file bench.py quotes as `traffic` was collected on the library
+    in this tree (lib_sha16 stamped by tools/pmc_label.py right after the
+    passes), labels every dispatch with the op bench.py filters on, and covers
+    the roofline workloads of round 4."""
+    h = bench.lib_sha16()
+    files = {v[0]: v[1] for v in bench.PMC_SUMMARIES.values()}
+    assert {w for w, _, _ in bench.PMC_SUMMARIES} >= {"rs10_4", "write14", "repair12", "files", "mixed16"}
+    for name, op in files.items():
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            doc = json.load(f)
+        assert doc["lib_sha16"] == h, (name, doc["lib_sha16"], h)
+        assert doc["dispatches"] and all(d["op"] == op for d in doc["dispatches"]), name
+
+
 def test_lib_hash_is_sixteen_hex_digits():
     h = bench.lib_sha16()
     assert len(h) == 16 and int(h, 16) >= 0

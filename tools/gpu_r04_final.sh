@@ -7,11 +7,12 @@
 #   pmc    FETCH_SIZE / WRITE_SIZE passes per workload, dispatches labelled
 #          with the bench line's bytes per launch -> pmc_<w>.json
 #   cfg    secondary workloads                    -> configs.jsonl
+#   probes StripeBatch staging layouts, multi-file batch shapes -> stripe_batch_layout.log, files_mix.log
 # STEPS selects (default: all).
 set -u
 OUT=gpurun_out
 mkdir -p $OUT
-STEPS=${STEPS:-"tests bench prof pmc cfg"}
+STEPS=${STEPS:-"tests bench prof pmc cfg probes"}
 has() { case " $STEPS " in *" $1 "*) return 0;; esac; return 1; }
 stop() { echo "STOP after $1 (rc=$2)"; exit $2; }
 nproc > $OUT/host.txt; lscpu | grep -E "Model name|^CPU\(s\)|NUMA" >> $OUT/host.txt
@@ -62,5 +63,11 @@ if has cfg; then
     cat $OUT/cfg.json >> $OUT/configs.jsonl
     python3 -c "import json; d=json.load(open('$OUT/cfg.json')); print('$w $extra', d['ms_per_step'], d['roofline']['frac'], d['verified'])"
   done
+fi
+if has probes; then
+  timeout -k 10 300 python3 tools/stripe_batch_layout_probe.py > $OUT/stripe_batch_layout.log 2>&1 || stop layout_probe $?
+  cat $OUT/stripe_batch_layout.log
+  timeout -k 10 300 python3 tools/files_mix_probe.py full10 ragged mix > $OUT/files_mix.log 2>&1 || stop files_mix $?
+  cat $OUT/files_mix.log
 fi
 echo ALL-DONE
