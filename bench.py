@@ -256,10 +256,15 @@ def load_traffic(args, wl_name, launch_bytes):
 class Workload:
     """One bench step = the ops in `ops`, each (label, fn(step_index), algorithmic bytes)."""
 
-    def __init__(self, name, metric, config, ops, buffers, roof_kernel, stripes, roof_ops=1, erase=None):
+    def __init__(self, name, metric, config, ops, buffers, roof_kernel, stripes, roof_ops=1, erase=None,
+                 roof_bytes=None, kernel_timer=None):
         self.name, self.metric, self.config, self.ops = name, metric, config, ops
         self.buffers, self.roof_kernel, self.stripes = buffers, roof_kernel, stripes
         self.roof_ops = roof_ops  # the first roof_ops ops are launches of the roofline kernel
+        # when an op launches more than the roofline kernel: that kernel's own
+        # algorithmic bytes per launch, and (start(), read() -> (ms, launches))
+        # timing it with HIP events inside the library
+        self.roof_bytes, self.kernel_timer = roof_bytes, kernel_timer
         # erase-and-rebuild checks run after the timed region: [(label, erase(), rebuild())] on buffers[0]
         self.erase = erase or []
 
@@ -505,19 +510,29 @@ def wl_files(args, ctx, stream, rank):
     # the partial data chunk is written, zero-padded, to the tail arena
     tail_written = sum((cl + 15) // 16 * 16 for (ns, nf, cl), L in zip(layouts, lengths)
                        if ns > nf and (L - nf * k * M) % cl)
+    # k_files_md5's own bytes per launch: every request's k data chunks read
+    # (last stripes: the whole ones from the object, the partial and all-zero
+    # ones from their tail slots, written there by the pad copy launched just
+    # before) and p parity chunks written, at the request's chunk length
+    kernel_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts)
     longest, nreq = files_longest_slot(n, k, M, lengths)
+    # NXEC_OBJECTS_ASYNC: the host plans batch i + 1 while batch i codes (the
+    # timed region ends with a stream sync)
     ops = [("encode_objects_md5",
             lambda i: ctx.encode_objects(n, k, ptrs, lengths, M, par.ptr, tail.ptr, md5.ptr, stream,
-                                         flags=nxec.OBJECTS_TAIL_INPLACE),
+                                         flags=nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC),
             user + parity_bytes + tail_written)]
     config = {"workload": f"{len(lengths)} files, sizes uniform in [1 B, {2 * k} MiB], RS({n},{k}) {M >> 10} KiB max "
                           f"chunks ({total} stripes, {user / 2**30:.1f} GiB user data): encode + MD5 of all chunks",
               "files": len(lengths), "stripes": total, "user_bytes": user, "requests": nreq,
               "tail": "nxec_encode_objects_ex(NXEC_OBJECTS_TAIL_INPLACE): whole last-stripe data chunks stay in "
                       "their objects, the partial one is written zero-padded",
-              "byte_accounting": "HBM side, the write14 convention: data read + parity written + tail-arena "
-                                 f"writes ({user / 2**30:.1f} + {parity_bytes / 2**30:.1f} + "
-                                 f"{tail_written / 2**30:.1f} GiB); the MD5 of every chunk reads LDS",
+              "byte_accounting": "value: HBM side of the call, the write14 convention: data read + parity "
+                                 f"written + tail-arena writes ({user / 2**30:.1f} + {parity_bytes / 2**30:.1f} + "
+                                 f"{tail_written / 2**30:.1f} GiB), the MD5 of every chunk reads LDS; roofline: "
+                                 f"k_files_md5 alone, (k + p) x chunk length per request ({kernel_bytes / 2**30:.2f} "
+                                 "GiB), timed by HIP events around its launch inside the library",
+              "host": "nxec_encode_objects_ex(NXEC_OBJECTS_ASYNC): the host plan of step i + 1 overlaps step i",
               "md5_chain_floor": {"longest_slot_steps": longest, "us_per_step": round(MD5_STEP_US, 3),
                                   "ms": round(longest * MD5_STEP_US / 1e3, 2),
                                   "note": "one lane's MD5 chain per chunk, a slot's requests back to back: the "
@@ -525,8 +540,10 @@ def wl_files(args, ctx, stream, rank):
                                           "(profiles/r02_encode_md5_role_probes.log)"}}
     return Workload("files", "GiB/s multi-file write (encode+MD5), RS(10,4), 1 MiB max chunk, device-resident",
                     config, ops, [arena, par, tail, md5],
-                    "encode_objects_ex(TAIL_INPLACE): one k_files_md5 launch, last stripes read from their objects, "
-                    "only their partial data chunks written to the tail arena", total)
+                    "k_files_md5<10> (encode_objects_ex(TAIL_INPLACE | ASYNC): after one small k_pad_chunks launch "
+                    "for the last stripes' partial chunks, one k_files_md5 launch codes and hashes every stripe)",
+                    total, roof_bytes=kernel_bytes,
+                    kernel_timer=(lambda: ctx.kernel_timing(True), ctx.kernel_time))
 
 
 CONFIG1 = ((6, 4, 1 << 20, "RS(4,2) read as (n,k)=(6,4), 4 MiB file, 1 MiB chunks"),
@@ -738,6 +755,8 @@ def main():
     evs = [[nxec.Event() for _ in range(nops + 1)] for _ in range(args.steps)]
     grp.barrier()
     nxec.device_sync()
+    if wl.kernel_timer:
+        wl.kernel_timer[0]()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, evs[i])
@@ -779,6 +798,11 @@ def main():
         ro = wl.ops[:wl.roof_ops]
         b0 = sum(b for _, _, b in ro) // len(ro)
         ms0 = sum(op_ms[:wl.roof_ops]) / len(ro)
+        kt = None
+        if wl.kernel_timer:
+            kms, kn = wl.kernel_timer[1]()
+            kt = {"launches": kn, "source": "nxec_kernel_time: HIP events inside libnxec around the kernel's launch"}
+            b0, ms0 = wl.roof_bytes, kms / max(kn, 1)
         gbs0 = b0 / (ms0 * 1e-3) / 1e9
         traffic, traffic_src = load_traffic(args, wl.name, b0)
         result = {
@@ -815,6 +839,8 @@ def main():
                            "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                     for (name, _, b), ms in zip(wl.ops, op_ms)},
         }
+        if kt:
+            result["roofline"]["kernel_timing"] = kt
         if ceiling:
             result["roofline"]["on_box_ceiling"] = ceiling
         if wl.name == "rs10_4":

@@ -387,9 +387,26 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
  * (the one-launch path leaves them alone: k_files_md5 then writes ~1/k of
  * the tail bytes). */
 #define NXEC_OBJECTS_TAIL_INPLACE 1
+/* NXEC_OBJECTS_ASYNC: return once the work is queued on `stream` (NULL: the
+ * context's) instead of when it is done.  lengths[] and d_objects[] (host
+ * arrays) may be reused at once; the objects, d_parity, d_tail and d_md5 are
+ * in use until the stream gets past the call.  A batching ChunkManager plans
+ * batch i + 1 on the host while batch i codes: its staging slot returns to
+ * the context's pool with an event the next user of that slot waits on (up
+ * to 4 calls in flight per context before one waits). */
+#define NXEC_OBJECTS_ASYNC 2
 int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsigned char *const *d_objects,
                            const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
                            unsigned char *d_tail, unsigned char *d_md5, int flags, void *stream);
+
+/* Device time of the coding launches of nxec_encode_objects(_ex) calls on ctx
+ * (roofline measurement: HIP events on the launch stream around the call's
+ * coding kernel -- k_files_md5 on the one-launch path; the pad copy, gather
+ * launches and MD5 launch together on the separate path).  nxec_kernel_timing
+ * turns it on (1) or off (0) and resets the totals; nxec_kernel_time waits for
+ * the pending launches and returns the milliseconds and launches since. */
+int nxec_kernel_timing(nxec_ctx_t *ctx, int enable);
+int nxec_kernel_time(nxec_ctx_t *ctx, double *ms, int64_t *launches);
 
 /* Host-inclusive form of nxec_encode_object: the object, parity
  * ([nstripes][n-k][M]) and digests ([nstripes][n][16], NULL = skip) are in

@@ -73,6 +73,8 @@ _PROTOS = {
     "nxec_encode_object_host": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, vp, vp, i64]),
     "nxec_objects_layout": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, i64, C.POINTER(i64), C.POINTER(i64)]),
     "nxec_encode_objects": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, i64, vp, vp, vp, vp]),
+    "nxec_kernel_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "nxec_kernel_time": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "nxec_encode_objects_ex": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
     "nxec_decode_object": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, vp, vp, vp]),
     "nxec_decode_object_ex": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, i64, vp, vp, vp]),

@@ -76,6 +76,12 @@ struct Slot {
   uint8_t *d = nullptr;
   size_t cap = 0;
   std::vector<hipEvent_t> events;  // per-piece completion (pipelined host path)
+  // asynchronous calls (NXEC_OBJECTS_ASYNC) hand the slot back while their
+  // launches still read its tables: recorded on the call's stream, waited on
+  // before the next user writes the staging
+  hipEvent_t busy = nullptr;
+  bool busy_set = false;
+  bool idle() const { return !busy_set || hipEventQuery(busy) == hipSuccess; }
 };
 
 // Host worker pool for staging copies (pageable <-> pinned) of the host entry
@@ -277,6 +283,12 @@ struct nxec_ctx {
   std::deque<struct DigestJob *> dg_pending;
   bool dg_leader = false;
   int dg_inflight = 0;
+  // nxec_kernel_timing: event pairs around the coding launches, read by nxec_kernel_time
+  std::mutex kt_mu;
+  bool kt_on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> kt_pending;
+  double kt_ms = 0;
+  int64_t kt_launches = 0;
 };
 
 // one nxec_encode_host_md5 call whose buffers are all device-mapped
@@ -326,15 +338,27 @@ int ensure_device(int device) {
 
 bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// staging slots a context grows to before an asynchronous caller waits for
+// one of its earlier calls (two in flight keep the GPU fed: the host plans
+// call i + 1 while call i runs)
+constexpr size_t kAsyncSlots = 4;
+
 int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
   Slot *s = nullptr;
   {
     // best fit: the smallest free slot that holds `bytes`, else the largest
     // (grown below) -- so callers of different sizes do not keep re-pinning
     // each other's slots (hipHostMalloc of a GiB costs ~0.1 s)
+    // (slots still read by an asynchronous call's launches only when no idle
+    // one is free and the context already has kAsyncSlots: then the best of
+    // those, waited on below)
     std::lock_guard<std::mutex> lk(ctx->slot_mu);
     int best = -1;
+    bool any_idle = false;
+    for (Slot *f : ctx->free_slots) any_idle = any_idle || f->idle();
+    const bool only_idle = any_idle || ctx->all_slots.size() < kAsyncSlots;
     for (int i = 0; i < static_cast<int>(ctx->free_slots.size()); i++) {
+      if (only_idle && !ctx->free_slots[i]->idle()) continue;
       const size_t c = ctx->free_slots[i]->cap;
       if (best < 0) {
         best = i;
@@ -357,6 +381,10 @@ int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
     }
     std::lock_guard<std::mutex> lk(ctx->slot_mu);
     ctx->all_slots.push_back(s);
+  }
+  if (s->busy_set) {  // an asynchronous call's launches may still read the staging
+    (void)hipEventSynchronize(s->busy);
+    s->busy_set = false;
   }
   if (s->cap < bytes) {
     if (s->h) (void)hipHostFree(s->h);
@@ -403,6 +431,8 @@ void release_slot(nxec_ctx_t *ctx, Slot *s) {
     }
   }
   (void)hipStreamSynchronize(s->stream);
+  if (s->busy_set) (void)hipEventSynchronize(s->busy);
+  s->busy_set = false;
   if (s->h) (void)hipHostFree(s->h);
   if (s->d) (void)hipFree(s->d);
   s->h = nullptr;
@@ -593,6 +623,11 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   ctx->obj.release();  // before the context stream it borrows
+  for (auto &pr : ctx->kt_pending) {
+    (void)hipEventSynchronize(pr.second);
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
   if (ctx->stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -603,6 +638,10 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
       (void)hipStreamDestroy(s->stream);
     }
     for (hipEvent_t ev : s->events) (void)hipEventDestroy(ev);
+    if (s->busy) {
+      (void)hipEventSynchronize(s->busy);
+      (void)hipEventDestroy(s->busy);
+    }
     if (s->h) (void)hipHostFree(s->h);
     if (s->d) (void)hipFree(s->d);
     delete s;
@@ -611,6 +650,77 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
 }
 
 void *nxec_ctx_stream(nxec_ctx_t *ctx) { return ctx ? static_cast<void *>(ctx->stream) : nullptr; }
+
+namespace {
+// an event pair around a coding launch when nxec_kernel_timing is on (else nulls)
+void kt_begin(nxec_ctx_t *ctx, hipStream_t st, hipEvent_t ev[2]) {
+  ev[0] = ev[1] = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(ctx->kt_mu);
+    if (!ctx->kt_on) return;
+  }
+  if (hipEventCreate(&ev[0]) != hipSuccess) {
+    ev[0] = nullptr;
+    return;
+  }
+  if (hipEventCreate(&ev[1]) != hipSuccess) {
+    (void)hipEventDestroy(ev[0]);
+    ev[0] = ev[1] = nullptr;
+    return;
+  }
+  (void)hipEventRecord(ev[0], st);
+}
+
+void kt_end(nxec_ctx_t *ctx, const hipEvent_t ev[2], hipStream_t st) {
+  if (!ev[0]) return;
+  (void)hipEventRecord(ev[1], st);
+  std::lock_guard<std::mutex> lk(ctx->kt_mu);
+  ctx->kt_pending.emplace_back(ev[0], ev[1]);
+}
+}  // namespace
+
+int nxec_kernel_timing(nxec_ctx_t *ctx, int enable) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  double ms = 0;
+  int64_t n = 0;
+  int rc = nxec_kernel_time(ctx, &ms, &n);  // drains (and frees) the pending pairs
+  std::lock_guard<std::mutex> lk(ctx->kt_mu);
+  ctx->kt_on = enable != 0;
+  ctx->kt_ms = 0;
+  ctx->kt_launches = 0;
+  return rc;
+}
+
+int nxec_kernel_time(nxec_ctx_t *ctx, double *ms, int64_t *launches) {
+  if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pend;
+  {
+    std::lock_guard<std::mutex> lk(ctx->kt_mu);
+    pend.swap(ctx->kt_pending);
+  }
+  double sum = 0;
+  int64_t cnt = 0;
+  int rc = NXEC_OK;
+  for (auto &pr : pend) {
+    float t = 0;
+    hipError_t e = hipEventSynchronize(pr.second);
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, pr.first, pr.second);
+    if (e == hipSuccess) {
+      sum += t;
+      cnt++;
+    } else if (!rc) {
+      rc = hip_err(e, "nxec_kernel_time");
+    }
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  std::lock_guard<std::mutex> lk(ctx->kt_mu);
+  ctx->kt_ms += sum;
+  ctx->kt_launches += cnt;
+  if (ms) *ms = ctx->kt_ms;
+  if (launches) *launches = ctx->kt_launches;
+  return rc;
+}
 
 int nxec_stripes_mul(nxec_ctx_t *ctx, int rows, int k, const unsigned char *coeffs, const unsigned char *d_src,
                      const int32_t *src_idx, int64_t src_chunk_stride, int64_t src_stripe_stride,
@@ -973,7 +1083,9 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
                            const int64_t *lengths, int64_t max_chunk_size, unsigned char *d_parity,
                            unsigned char *d_tail, unsigned char *d_md5, int flags, void *stream) {
   if (!ctx) return set_error(NXEC_ERR_INVALID, "null context");
-  if (flags & ~NXEC_OBJECTS_TAIL_INPLACE) return set_error(NXEC_ERR_INVALID, "nxec_encode_objects_ex: flags %d", flags);
+  if (flags & ~(NXEC_OBJECTS_TAIL_INPLACE | NXEC_OBJECTS_ASYNC))
+    return set_error(NXEC_ERR_INVALID, "nxec_encode_objects_ex: flags %d", flags);
+  const bool async = flags & NXEC_OBJECTS_ASYNC;
   // NXEC_TIMING=1: the host side's share of the call on stderr (planning, tables, launch, wait)
   static const bool timing = [] {
     const char *e = std::getenv("NXEC_TIMING");
@@ -1214,6 +1326,7 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   if (rc) return rc;
   // the slot's staging may still be in use by an earlier call on its own stream
   rc = hip_check(hipStreamSynchronize(slot->stream), "slot sync");
+  if (!rc && async && !slot->busy) rc = hip_check(hipEventCreateWithFlags(&slot->busy, hipEventDisableTiming), "slot event");
   for (int i = 0; i < kTabs && !rc; i++)
     if (tabs[i].bytes) std::memcpy(slot->h + off[i], tabs[i].h, tabs[i].bytes);
   if (!rc) rc = hip_check(hipMemcpyAsync(slot->d, slot->h, off[kTabs], hipMemcpyHostToDevice, st), "tables H2D");
@@ -1251,8 +1364,20 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
       (void)hipMemsetAsync(d_clock, 0, size_t(nwg) * 3 * 8, st);
       fa.wg_clock = d_clock;
     }
-    if (!rc) rc = launch_files_md5(fa, ctx->num_cus, st);
+    if (!rc) {
+      hipEvent_t kt[2];
+      kt_begin(ctx, st, kt);
+      rc = launch_files_md5(fa, ctx->num_cus, st);
+      kt_end(ctx, kt, st);
+    }
     const double t_launch = timing ? ms_since(th0) : 0;
+    if (async && !d_clock) {  // the tables stay in the slot until the stream gets past the launches
+      if (!rc) rc = hip_check(hipEventRecord(slot->busy, st), "slot event record");
+      slot->busy_set = !rc;
+      if (rc) (void)hipStreamSynchronize(st);
+      release_slot(ctx, slot);
+      return rc;
+    }
     const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
     if (d_clock) {  // per workgroup: start, code end, hash end (100 MHz), by slot composition
       std::vector<unsigned long long> c(size_t(nwg) * 3);
@@ -1279,6 +1404,8 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
     release_slot(ctx, slot);
     return rc ? rc : rc2;
   }
+  hipEvent_t kt[2];
+  kt_begin(ctx, st, kt);
   if (!rc && p > 0 && full_aligned && nfs > 0)
     rc = stripes_mul_impl(ctx, p, k, prow, nullptr, reinterpret_cast<const unsigned char *const *>(dptr(0)), nullptr,
                           0, 0, nullptr, reinterpret_cast<unsigned char *const *>(dptr(1)), nullptr, 0, 0, nullptr, M,
@@ -1296,6 +1423,14 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
                          reinterpret_cast<const int64_t *>(dptr(8)), int64_t(ulist.size()), uprefix.back(),
                          ctx->num_cus, st);
   if (!rc && !items.empty()) rc = launch_md5_list(reinterpret_cast<const Md5Item *>(dptr(9)), int64_t(items.size()), st);
+  kt_end(ctx, kt, st);
+  if (async) {
+    if (!rc) rc = hip_check(hipEventRecord(slot->busy, st), "slot event record");
+    slot->busy_set = !rc;
+    if (rc) (void)hipStreamSynchronize(st);
+    release_slot(ctx, slot);
+    return rc;
+  }
   // the tables live in the slot: drain before handing it back (synchronous call)
   const int rc2 = hip_check(hipStreamSynchronize(st), "nxec_encode_objects sync");
   release_slot(ctx, slot);

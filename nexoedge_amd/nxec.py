@@ -82,6 +82,7 @@ def decode_matrix(n: int, k: int, input_ids: Sequence[int], targets: Sequence[in
 
 LAYOUT_RECOVER_HEAVY = 1
 OBJECTS_TAIL_INPLACE = 1  # nxec_encode_objects_ex: only the partial last-stripe chunk to the tail arena
+OBJECTS_ASYNC = 2  # nxec_encode_objects_ex: return once queued on the stream
 
 
 def batch_layout(n: int, length: int, flags: int = 0):
@@ -469,13 +470,24 @@ class Context:
     def encode_objects(self, n: int, k: int, objects: Sequence[int], lengths: Sequence[int], max_chunk_size: int,
                        parity: int, tail=None, md5=None, stream=None, flags: int = 0) -> None:
         """nxec_encode_objects_ex; flags = OBJECTS_TAIL_INPLACE writes only each
-        last stripe's partial data chunk to the tail arena (include/nxec.h)."""
+        last stripe's partial data chunk to the tail arena, OBJECTS_ASYNC returns
+        once the work is queued on the stream (include/nxec.h)."""
         ptrs = (C.c_void_p * max(len(objects), 1))(*[int(o) if o else None for o in objects])
         ln = np.ascontiguousarray(np.asarray(list(lengths), dtype=np.int64))
         check(lib.nxec_encode_objects_ex(C.c_void_p(self.ptr), n, k, len(ln), ptrs, C.c_void_p(ln.ctypes.data),
                                          max_chunk_size, C.c_void_p(int(parity)),
                                          C.c_void_p(int(tail) if tail else None),
                                          C.c_void_p(int(md5) if md5 else None), flags, stream), "nxec_encode_objects")
+
+    def kernel_timing(self, enable: bool = True) -> None:
+        """nxec_kernel_timing: event-time the coding launches of encode_objects (totals reset)."""
+        check(lib.nxec_kernel_timing(C.c_void_p(self.ptr), int(enable)), "nxec_kernel_timing")
+
+    def kernel_time(self):
+        """nxec_kernel_time: (milliseconds, launches) since kernel_timing()."""
+        ms, n = C.c_double(), C.c_int64()
+        check(lib.nxec_kernel_time(C.c_void_p(self.ptr), C.byref(ms), C.byref(n)), "nxec_kernel_time")
+        return ms.value, n.value
 
     def encode_object_host(self, n: int, k: int, obj: int, length: int, max_chunk_size: int, parity: int,
                            md5=None, batch_stripes: int = 0) -> None:

@@ -1400,6 +1400,65 @@ def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
     arena.free()
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_encode_objects_async_pipeline(gpu_ctx, monkeypatch, fused):
+    """NXEC_OBJECTS_ASYNC (include/nxec.h): six different batches queued back to
+    back on the context stream -- more than the context's four staging slots,
+    so later calls wait for earlier ones' slots -- equal the synchronous calls'
+    parity, tails and digests; the host length arrays are rebuilt between calls
+    (the call consumed them).  nxec_kernel_time counts one timed launch per call
+    with a positive device time.  fused = 0: the separate launches
+    (NXEC_FUSED_MD5=0) take the same asynchronous exit."""
+    monkeypatch.setenv("NXEC_FUSED_MD5", fused)
+    n, k, M = 14, 10, 16384
+    p = n - k
+    batches = []
+    for b in range(6):
+        rng = np.random.default_rng(900 + b)
+        lengths = [int(x) for x in rng.integers(1, 2 * k * M + 1, size=64 + 37 * b)]
+        offs = np.concatenate([[0], np.cumsum([(L + 15) // 16 * 16 for L in lengths])])
+        arena = up(rng.integers(0, 256, size=int(offs[-1]) + 16, dtype=np.uint8))
+        total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+        batches.append((lengths, [arena.ptr + int(o) for o in offs[:-1]], total, tail_bytes, arena))
+
+    def outputs(flags, timing=False):
+        bufs = []
+        if timing:
+            gpu_ctx.kernel_timing(True)
+        for lengths, ptrs, total, tail_bytes, _ in batches:
+            par, tail, md5 = (nxec.DeviceBuffer(total * p * M), nxec.DeviceBuffer(max(tail_bytes, 16)),
+                              nxec.DeviceBuffer(total * n * 16))
+            tail.memset(0)
+            gpu_ctx.encode_objects(n, k, ptrs, list(lengths), M, par.ptr, tail.ptr, md5.ptr, flags=flags)
+            bufs.append((par, tail, md5))
+        gpu_ctx.sync()
+        kt = gpu_ctx.kernel_time() if timing else None
+        if timing:
+            gpu_ctx.kernel_timing(False)
+        out = [tuple(b.download() for b in t) for t in bufs]
+        for t in bufs:
+            for b in t:
+                b.free()
+        return out, kt
+
+    want, _ = outputs(nxec.OBJECTS_TAIL_INPLACE)
+    got, (ms, launches) = outputs(nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC, timing=True)
+    assert launches == len(batches) and ms > 0
+    for (lengths, _, total, _, _), w, g in zip(batches, want, got):
+        assert np.array_equal(w[2], g[2])  # digests
+        pw, pg = w[0].reshape(total, p, M), g[0].reshape(total, p, M)
+        s0 = 0
+        for L in lengths:
+            ns, nf, cl = nxec.object_layout(n, k, L, M)
+            for s in range(ns):
+                cs = M if s < nf else cl
+                assert np.array_equal(pw[s0 + s, :, :cs], pg[s0 + s, :, :cs])
+            s0 += ns
+        assert np.array_equal(w[1], g[1])  # tail slots the calls wrote (the rest stayed zero in both)
+    for b in batches:
+        b[4].free()
+
+
 @pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 700), (14, 10, 65536, 300), (6, 4, 1000 * 16, 200),
                                           (20, 16, 2048, 5000)])
 def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
