@@ -520,10 +520,11 @@ constexpr int gm_depth() {
 }
 // k_files_md5 reads HBM (a step of ~2 us is many load latencies), and its
 // last-stripe path needs registers of its own: at most 3 steps in flight,
-// 2 from k = 13 (no spills through k = 16)
-template <int K>
+// 2 from k = 13 (no spills through k = 16); without that path (TAIL = false)
+// k_mul_md5's depth
+template <int K, bool TAIL = true>
 constexpr int fm_depth() {
-  return K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
+  return !TAIL ? em_depth<K>() : K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
 }
 
 // The agent's requests (container_manager.cc:221-258 partial encodes and
@@ -715,7 +716,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 // as k_mul_md5's: bit 0 no MD5 rounds, bit 1 no table lookups, bit 2 no
 // global loads or stores, bit 3 (alone, 8) no tail-arena stores, bit 4
 // (alone, 16) last stripes coded like whole stripes (no tail handling).
-template <int K, int PROBE = 0>
+// TAIL = false: no request reads a last stripe from its object (a.tail_src is
+// null: in place, last stripes are ordinary requests) -- every tail branch,
+// its state and its registers compile out of the step loop.
+template <int K, int PROBE = 0, bool TAIL = true>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = K + a.p;
@@ -792,8 +796,8 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // parity chunk -- and row bytes the hash lanes mask off)
     auto tail_state = [&](int li, int64_t cl, uint32_t &tl, uint32_t &jf, uint32_t &last, const uint8_t *&end,
                           uint32_t &jc, uint32_t &zf) {
-      const uint64_t tb = act ? q[li * rec + K + a.p + 2] : uint64_t(0);
-      const int64_t rem = act ? static_cast<int64_t>(q[li * rec + K + a.p + 3]) : int64_t(0);
+      const uint64_t tb = TAIL && act ? q[li * rec + K + a.p + 2] : uint64_t(0);
+      const int64_t rem = TAIL && act ? static_cast<int64_t>(q[li * rec + K + a.p + 3]) : int64_t(0);
       const int64_t f = tb && cl > 0 ? min(rem / cl, static_cast<int64_t>(K)) : 0;
       tl = tb ? static_cast<uint32_t>(cl) : 0u;
       jf = static_cast<uint32_t>(f);
@@ -812,7 +816,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // the request (chunks under 256 bytes) -- the scratch line: nothing past a
     // chunk's 16-byte padding is read
     auto set_src = [&](int li, bool has) {
-      const uint64_t tb = act ? q[li * rec + K + a.p + 2] : uint64_t(0);
+      const uint64_t tb = TAIL && act ? q[li * rec + K + a.p + 2] : uint64_t(0);
       const int64_t cl = len_of(li);
 #pragma unroll
       for (int j = 0; j < K; j++)
@@ -826,7 +830,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     tail_state(0, len0, ltl, ljf, llast, lend, ljc, lzf);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
-      const bool wtl = !(PROBE & 16) && __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
+      const bool wtl = TAIL && !(PROBE & 16) && __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
 #pragma unroll
       for (int j = 0; j < K; j++) {
         // a tail chunk's 16 bytes are read where they lie (global loads take
@@ -876,8 +880,8 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     const uint8_t *cend = lend;
     // the tail source and the tail arena's chunk 0 (chunk j at + j*cls), kept
     // in registers: no per-step read of the request table
-    const uint8_t *ctb = act ? reinterpret_cast<const uint8_t *>(q[K + a.p + 2]) : nullptr;
-    uint8_t *ctd = act ? reinterpret_cast<uint8_t *>(q[0]) : nullptr;
+    const uint8_t *ctb = TAIL && act ? reinterpret_cast<const uint8_t *>(q[K + a.p + 2]) : nullptr;
+    uint8_t *ctd = TAIL && act ? reinterpret_cast<uint8_t *>(q[0]) : nullptr;
     uint8_t *dp[kMaxRowsPerPass];
     auto set_dst = [&](int li) {
 #pragma unroll
@@ -917,7 +921,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
       const bool tl = live && ctl != 0;
-      const bool wtc = !(PROBE & 16) && __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
+      const bool wtc = TAIL && !(PROBE & 16) && __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
       if (wtc) {
         // wait for this step's loads here, in uniform control flow: a first
         // use inside the per-lane tail branches below would be counted
@@ -984,14 +988,16 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           ctmax = tmax_of(ln);
           set_dst(cr);
           tail_state(cr, ln, ctl, cjf, clast, cend, cjc, czf);
-          ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
-          ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
+          if (TAIL) {
+            ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
+            ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
+          }
         } else {
           live = false;
         }
       }
     };
-    constexpr int D = fm_depth<K>();
+    constexpr int D = fm_depth<K, TAIL>();
     u32x4 ring[D][K];
 #pragma unroll
     for (int j = 0; j < D - 1; j++) load(ring[j]);
@@ -1124,6 +1130,12 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int
   return {{&k_files_md5<Ks + 1>...}};
 }
 const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+template <int... Ks>
+constexpr std::array<FmKernel, sizeof...(Ks)> fm_table_nt(std::integer_sequence<int, Ks...>) {
+  return {{&k_files_md5<Ks + 1, 0, false>...}};
+}
+// no request with a tail source (in place): the tail-free step loop
+const std::array<FmKernel, kFilesMd5MaxK> kFmNt = fm_table_nt(std::make_integer_sequence<int, kFilesMd5MaxK>{});
 #if NXEC_DESIGN_PROBES
 // bit 3 alone: no tail-arena stores (everything else as the product);
 // bit 4 alone: last stripes read straight from the object like whole
@@ -1188,7 +1200,9 @@ int prepare_encode_md5() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_mul_md5): %s", hipGetErrorString(e));
   }
-  for (FmKernel fn : kFm) {
+  std::vector<FmKernel> fms(kFm.begin(), kFm.end());
+  fms.insert(fms.end(), kFmNt.begin(), kFmNt.end());
+  for (FmKernel fn : fms) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
       return set_error(NXEC_ERR_HIP, "k_files_md5: static LDS present (the tables must start at LDS byte 0)");
@@ -1378,7 +1392,7 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
   const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
-  FmKernel fn = kFm[a.k - 1];
+  FmKernel fn = a.tail_src ? kFm[a.k - 1] : kFmNt[a.k - 1];
 #if NXEC_DESIGN_PROBES
   if (const char *e = std::getenv("NXEC_FM_PROBE"))
     if (a.k == 10)

@@ -1339,8 +1339,11 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
     if (!rc && !pads.empty())
       rc = launch_pad_chunks(reinterpret_cast<const PadChunks *>(dptr(2)), reinterpret_cast<const uint32_t *>(dptr(3)),
                              int64_t(pads.size()), pad_blocks, st);
-    fa.tail_src = reinterpret_cast<const uint8_t *const *>(slot->d + off[8]);
-    fa.tail_rem = reinterpret_cast<const int64_t *>(slot->d + off[9]);
+    // no last stripe read from its object (in place: all ordinary requests):
+    // null tables select the kernel without the tail handling
+    const bool any_tail = std::any_of(f_tsrc.begin(), f_tsrc.end(), [](const uint8_t *t) { return t != nullptr; });
+    fa.tail_src = any_tail ? reinterpret_cast<const uint8_t *const *>(slot->d + off[8]) : nullptr;
+    fa.tail_rem = any_tail ? reinterpret_cast<const int64_t *>(slot->d + off[9]) : nullptr;
     fa.src_ptrs = reinterpret_cast<const uint8_t *const *>(slot->d + off[0]);
     fa.dst_ptrs = reinterpret_cast<uint8_t *const *>(slot->d + off[1]);
     fa.lens = reinterpret_cast<const int64_t *>(slot->d + off[2]);
