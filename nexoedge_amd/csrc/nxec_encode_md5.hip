@@ -521,10 +521,11 @@ constexpr int gm_depth() {
 // k_files_md5 reads HBM (a step of ~2 us is many load latencies), and its
 // last-stripe path needs registers of its own: at most 3 steps in flight,
 // 2 from k = 13 (no spills through k = 16); without that path (TAIL = false)
-// k_mul_md5's depth
+// up to 4 as k_mul_md5, as the 64-bit source pointers leave room (4 through
+// k = 11, 3 through 14, then 2)
 template <int K, bool TAIL = true>
 constexpr int fm_depth() {
-  return !TAIL ? em_depth<K>() : K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
+  return !TAIL ? (gm_depth<K>() > 4 ? 4 : gm_depth<K>()) : K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
 }
 
 // The agent's requests (container_manager.cc:221-258 partial encodes and
