@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnxec.so")
+# NXEC_LIB: another build of the library (design A/Bs of compile-time variants;
+# tools only -- the product and the tests load the in-tree build)
+LIB_PATH = os.environ.get("NXEC_LIB") or os.path.join(_HERE, "lib", "libnxec.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

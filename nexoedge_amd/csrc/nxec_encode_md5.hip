@@ -155,6 +155,9 @@ __device__ __forceinline__ void lookup_nib(int j, const u32x4 d, uint32_t lane4,
 // (the rest of the code role needs ~20 with buffer-resource addressing)
 template <int K>
 constexpr int em_depth() {
+#ifdef NXEC_EM_DEPTH  // design A/B of the ring depth (a separate build)
+  if (K == 10) return NXEC_EM_DEPTH;
+#endif
   return K * 4 * 4 <= 200 ? 4 : K * 4 * 3 <= 200 ? 3 : 2;
 }
 
