@@ -722,8 +722,10 @@ __global__ __launch_bounds__(kEmBlock) void k_gather_md5(const GatherMd5Args a) 
 // (alone, 16) last stripes coded like whole stripes (no tail handling).
 // TAIL = false: no request reads a last stripe from its object (a.tail_src is
 // null: in place, last stripes are ordinary requests) -- every tail branch,
-// its state and its registers compile out of the step loop.
-template <int K, int PROBE = 0, bool TAIL = true>
+// its state and its registers compile out of the step loop.  TSTORE (with
+// TAIL = false; a.tail_store): last stripes are in-place requests and the
+// code lanes also store their whole data chunks to the tail arena.
+template <int K, int PROBE = 0, bool TAIL = true, bool TSTORE = false>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = K + a.p;
@@ -922,8 +924,24 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       return u32x4{x.x & m[0], x.y & m[1], x.z & m[2], x.w & m[3]};
     };
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
+    // TSTORE: the compute request's tail slot 0 (nullptr: a full stripe), slot
+    // stride, whole chunks stored (j < sj0) and its chunk length
+    uint8_t *std_ = nullptr;
+    int64_t scls = 0;
+    int32_t sj0 = 0, scl = 0;
+    auto set_store = [&](int li) {
+      if (!TSTORE) return;
+      std_ = act ? reinterpret_cast<uint8_t *>(q[li * rec + K + a.p + 2]) : nullptr;
+      const uint64_t w = act ? q[li * rec + K + a.p + 3] : 0;
+      scls = static_cast<int64_t>(w & ((uint64_t(1) << 40) - 1));
+      sj0 = static_cast<int32_t>(w >> 40);
+      scl = static_cast<int32_t>(len_of(li));
+    };
+    set_store(0);
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
+      // wave-uniform: only waves holding a last stripe store
+      const bool wst = TSTORE && __builtin_amdgcn_ballot_w64(ok && std_ != nullptr) != 0;
       const bool tl = live && ctl != 0;
       const bool wtc = TAIL && !(PROBE & 16) && __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
       if (wtc) {
@@ -963,6 +981,19 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = x0;
           if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = x1;
         }
+        if (wst && ok && std_) {  // whole chunks to the tail arena, zero past the chunk's end
+          const int32_t nv = scl - pos;
+          uint32_t m[4];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int keep = nv - 4 * i;
+            m[i] = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+          }
+          if (j < sj0)
+            dev::st_global_stream(std_ + j * scls + pos, u32x4{x0.x & m[0], x0.y & m[1], x0.z & m[2], x0.w & m[3]});
+          if (j + 1 < K && j + 1 < sj0)
+            dev::st_global_stream(std_ + (j + 1) * scls + pos, u32x4{x1.x & m[0], x1.y & m[1], x1.z & m[2], x1.w & m[3]});
+        }
         if (PROBE & 2) {
           if (j == 0) acc[0] = x0.x, acc[5] = x0.y, acc[10] = x0.z, acc[15] = x0.w;
         } else {
@@ -996,6 +1027,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
             ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
             ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
           }
+          set_store(cr);
         } else {
           live = false;
         }
@@ -1140,6 +1172,12 @@ constexpr std::array<FmKernel, sizeof...(Ks)> fm_table_nt(std::integer_sequence<
 }
 // no request with a tail source (in place): the tail-free step loop
 const std::array<FmKernel, kFilesMd5MaxK> kFmNt = fm_table_nt(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+template <int... Ks>
+constexpr std::array<FmKernel, sizeof...(Ks)> fm_table_st(std::integer_sequence<int, Ks...>) {
+  return {{&k_files_md5<Ks + 1, 0, false, true>...}};
+}
+// in-place requests that also store last stripes' whole chunks to the tail arena
+const std::array<FmKernel, kFilesMd5MaxK> kFmSt = fm_table_st(std::make_integer_sequence<int, kFilesMd5MaxK>{});
 #if NXEC_DESIGN_PROBES
 // bit 3 alone: no tail-arena stores (everything else as the product);
 // bit 4 alone: last stripes read straight from the object like whole
@@ -1206,6 +1244,7 @@ int prepare_encode_md5() {
   }
   std::vector<FmKernel> fms(kFm.begin(), kFm.end());
   fms.insert(fms.end(), kFmNt.begin(), kFmNt.end());
+  fms.insert(fms.end(), kFmSt.begin(), kFmSt.end());
   for (FmKernel fn : fms) {
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
@@ -1396,7 +1435,8 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
   const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
-  FmKernel fn = a.tail_src ? kFm[a.k - 1] : kFmNt[a.k - 1];
+  FmKernel fn = a.tail_store ? kFmSt[a.k - 1] : a.tail_src ? kFm[a.k - 1] : kFmNt[a.k - 1];
+  if (a.tail_store && (!a.tail_src || !a.tail_rem)) return set_error(NXEC_ERR_INVALID, "files+md5: tail-store tables");
 #if NXEC_DESIGN_PROBES
   if (const char *e = std::getenv("NXEC_FM_PROBE"))
     if (a.k == 10)

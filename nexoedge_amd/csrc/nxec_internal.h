@@ -273,6 +273,12 @@ struct FilesMd5Args {
   // partial one (zero-padded) is written to the tail arena; the whole ones
   // stay where they are in the object, the all-zero ones are not written
   int32_t tail_partial_only;
+  // Whole tail arena with last stripes as in-place requests (no flag): the
+  // code lanes also store a last stripe's whole data chunks j < j0 -- read in
+  // place from the object -- to their tail slots, bytes past the chunk's
+  // length zeroed.  tail_src[s] = the tail arena's chunk 0 of request s
+  // (nullptr: a full stripe), tail_rem[s] = cls | j0 << 40
+  int32_t tail_store;
   // NXEC_FILES_CLOCK=1 (diagnostics): per workgroup, s_memrealtime at the
   // start, at the end of code wave 0 and at the end of hash wave 0
   unsigned long long *wg_clock;

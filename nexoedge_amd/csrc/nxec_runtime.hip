@@ -1155,7 +1155,16 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   const bool sep = !fused;
   const bool need_pads = sep || !tail_direct;
   // NXEC_OBJECTS_TAIL_INPLACE on the one-launch path (NXEC_FILES_TAIL=0 keeps the whole-tail pad copy)
-  const bool inplace = (flags & NXEC_OBJECTS_TAIL_INPLACE) && fused && tail_direct;
+  // Without the flag (whole tail arena) last stripes are in-place requests
+  // too, and the kernel also stores their whole data chunks to the tail
+  // arena (tail_store); NXEC_FILES_COPY=kernel: the kernel's older last-stripe
+  // path that reads the tail bytes itself (A/B)
+  static const bool copy_in_kernel = [] {
+    const char *e = std::getenv("NXEC_FILES_COPY");
+    return e && e[0] == 'k';
+  }();
+  const bool tstore = !(flags & NXEC_OBJECTS_TAIL_INPLACE) && fused && tail_direct && !copy_in_kernel;
+  const bool inplace = ((flags & NXEC_OBJECTS_TAIL_INPLACE) || tstore) && fused && tail_direct;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {
     int64_t ns = 0, nf = 0, cl = 0;
@@ -1231,8 +1240,9 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
           q_len.push_back(cl);
           q_dig.push_back(dig);
-          q_tsrc.push_back(nullptr);
-          q_trem.push_back(0);
+          // tail_store: the kernel writes chunks j < j0 (read in place) to their slots
+          q_tsrc.push_back(tstore ? td : nullptr);
+          q_trem.push_back(tstore ? (cls | (j0 << 40)) : 0);
         } else if (fused) {  // read from the object; the kernel writes the padded chunks to td
           for (int j = 0; j < k; j++) q_src.push_back(td + j * cls);
           for (int i = 0; i < p; i++) q_dst.push_back(par + i * M);
@@ -1355,6 +1365,7 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
     fa.k = k;
     fa.p = p;
     fa.tail_partial_only = 0;  // in place, last stripes reach the kernel as ordinary requests
+    fa.tail_store = tstore && any_tail ? 1 : 0;
     std::memcpy(fa.coef, prow, size_t(p) * k);
     // NXEC_FILES_CLOCK=1: per-workgroup timestamps (diagnostics, stderr)
     static const bool wg_clock = [] {
