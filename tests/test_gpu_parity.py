@@ -1459,6 +1459,79 @@ def test_encode_objects_async_pipeline(gpu_ctx, monkeypatch, fused):
         b[4].free()
 
 
+def test_encode_objects_async_threads(gpu_ctx):
+    """NXEC_OBJECTS_ASYNC from two threads on one context, each on its own
+    stream, four batches each back to back: the staging-slot pool (slots
+    handed back with a pending event, waited on by their next user) gives
+    every call its own tables -- outputs equal the synchronous calls'."""
+    import threading
+    n, k, M = 14, 10, 8192
+    p = n - k
+    jobs = []
+    for b in range(8):
+        rng = np.random.default_rng(1700 + b)
+        lengths = [int(x) for x in rng.integers(1, 3 * k * M, size=40 + 11 * b)]
+        offs = np.concatenate([[0], np.cumsum([(L + 15) // 16 * 16 for L in lengths])])
+        arena = up(rng.integers(0, 256, size=int(offs[-1]) + 16, dtype=np.uint8))
+        total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+        jobs.append((lengths, [arena.ptr + int(o) for o in offs[:-1]], total, tail_bytes, arena))
+
+    def outputs(job, flags, stream=None):
+        lengths, ptrs, total, tail_bytes, _ = job
+        bufs = (nxec.DeviceBuffer(total * p * M), nxec.DeviceBuffer(max(tail_bytes, 16)),
+                nxec.DeviceBuffer(total * n * 16))
+        bufs[1].memset(0)
+        gpu_ctx.encode_objects(n, k, ptrs, lengths, M, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, stream=stream,
+                               flags=flags)
+        return bufs
+
+    want = []
+    for job in jobs:
+        bufs = outputs(job, nxec.OBJECTS_TAIL_INPLACE)
+        want.append([b.download() for b in bufs])
+        for b in bufs:
+            b.free()
+    got = [None] * len(jobs)
+    errors = []
+
+    def worker(t):
+        try:
+            st = C.c_void_p()
+            check_rc = nxec._lib.lib.nxec_stream_create(C.byref(st))
+            assert check_rc == 0
+            mine = [(i, outputs(jobs[i], nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC, st.value))
+                    for i in range(t, len(jobs), 2)]
+            assert nxec._lib.lib.nxec_stream_sync(st) == 0
+            for i, bufs in mine:
+                got[i] = [b.download() for b in bufs]
+                for b in bufs:
+                    b.free()
+            nxec._lib.lib.nxec_stream_destroy(st)
+        except Exception as e:  # noqa: BLE001 -- re-raised in the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    for i, job in enumerate(jobs):
+        lengths, _, total, _, _ = job
+        assert np.array_equal(want[i][2], got[i][2]), i  # digests
+        pw, pg = want[i][0].reshape(total, p, M), got[i][0].reshape(total, p, M)
+        s0 = 0
+        for L in lengths:
+            ns, nf, cl = nxec.object_layout(n, k, L, M)
+            for s in range(ns):
+                cs = M if s < nf else cl
+                assert np.array_equal(pw[s0 + s, :, :cs], pg[s0 + s, :, :cs]), (i, s0 + s)
+            s0 += ns
+        assert np.array_equal(want[i][1], got[i][1]), i
+    for job in jobs:
+        job[4].free()
+
+
 @pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 700), (14, 10, 65536, 300), (6, 4, 1000 * 16, 200),
                                           (20, 16, 2048, 5000)])
 def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
