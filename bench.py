@@ -463,7 +463,7 @@ MD5_STEP_US = 9.8e3 / 4096
 
 def files_longest_slot(n, k, M, lengths, cus=256, step=256):
     """Steps of the longest slot of nxec_encode_objects' fused plan (the LPT of
-    plan_files_slots, nxec_encode_md5.hip, over every request: a file's full
+    plan_files_slots, nxec_files_md5.hip, over every request: a file's full
     stripes and its last stripe), and the request count."""
     import heapq
 

@@ -202,6 +202,8 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
                       const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off,
                       const uint32_t *copy_off = nullptr);
 int prepare_encode_md5();
+// k_files_md5's kernel attributes (nxec_files_md5.hip; called by prepare_encode_md5)
+int prepare_files_md5();
 int launch_mul_md5(const MulMd5Args &a, int num_cus, void *stream);
 
 // The agent's form of the fused kernel (nxec_agent_encode_batch): request s
