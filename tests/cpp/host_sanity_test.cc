@@ -9,7 +9,9 @@
 // NXEC_ERR_NODEV (or INVALID) and never crash, leak or race.
 //
 // Exit 0 iff every check passed.
+#include <algorithm>
 #include <atomic>
+#include <functional>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +27,7 @@
 #include "coding/coding_options.hh"
 #include "coding/coding_util.hh"
 #include "nxec.h"
+#include "nxec_internal.h"
 
 static std::atomic<int> g_fail{0};
 #define CHECK(cond, ...)            \
@@ -277,8 +280,79 @@ static void digest_pool(int t) {
   }
 }
 
+// The multi-file write's slot plan (nxec::plan_files_slots, host code of
+// nxec_encode_objects): random batches, lengths descending as the runtime
+// passes them.  Every request in exactly one slot, lists in request order,
+// per-workgroup step counts = the longest slot of the group, the LDS request
+// table fits, one request per slot while they fit one workgroup wave, and --
+// greedy least-loaded placement -- the longest slot within the longest
+// request of the average.
+static void files_slot_plan() {
+  std::mt19937_64 rng(20261017);
+  int bound_checked = 0;
+  for (int trial = 0; trial < 300; trial++) {
+    const int k = 1 + static_cast<int>(rng() % nxec::kFilesMd5MaxK), p = 1 + static_cast<int>(rng() % 4);
+    const int cus = trial % 3 == 0 ? 256 : 8 + static_cast<int>(rng() % 249);
+    const int R = 1 + static_cast<int>(rng() % (trial % 4 == 0 ? 9000 : 600));
+    const int64_t M = int64_t(1) << (12 + rng() % 9);  // 4 KiB .. 1 MiB chunks
+    std::vector<int64_t> lens(static_cast<size_t>(R));
+    for (auto &l : lens) l = rng() % 3 == 0 ? M : 1 + static_cast<int64_t>(rng() % static_cast<uint64_t>(M));
+    std::sort(lens.begin(), lens.end(), std::greater<int64_t>());
+    std::vector<int32_t> first, reqs, wg;
+    nxec::FilesMd5Args a;
+    std::memset(&a, 0, sizeof(a));
+    nxec::plan_files_slots(lens, k, p, cus, first, reqs, wg, a);
+    const int64_t G = a.nslots, S = a.slots_per_group, nh = k + p;
+    CHECK(G >= 1 && S >= 1 && S <= 16 && S * nh <= 256, "plan %d: slots %lld, per group %lld", trial,
+          static_cast<long long>(G), static_cast<long long>(S));
+    CHECK(static_cast<int64_t>(first.size()) == G + 1 && first[0] == 0 && first.back() == R, "plan %d: slot_first",
+          trial);
+    std::vector<int> seen(static_cast<size_t>(R), 0);
+    std::vector<int64_t> load(static_cast<size_t>(G), 0);
+    int maxl = 0;
+    int64_t total = 0, longest_req = 0;
+    for (int64_t g = 0; g < G; g++) {
+      CHECK(first[g + 1] >= first[g], "plan %d: slot %lld list", trial, static_cast<long long>(g));
+      maxl = std::max(maxl, first[g + 1] - first[g]);
+      for (int i = first[g]; i < first[g + 1]; i++) {
+        const int r = reqs[static_cast<size_t>(i)];
+        CHECK(r >= 0 && r < R, "plan %d: request %d", trial, r);
+        if (r < 0 || r >= R) continue;
+        seen[static_cast<size_t>(r)]++;
+        if (i > first[g]) CHECK(reqs[static_cast<size_t>(i - 1)] < r, "plan %d: slot list order", trial);
+        const int64_t st = (lens[static_cast<size_t>(r)] + nxec::kEncMd5Step - 1) / nxec::kEncMd5Step;
+        load[static_cast<size_t>(g)] += st;
+        total += st;
+        longest_req = std::max(longest_req, st);
+      }
+    }
+    for (int r = 0; r < R; r++) CHECK(seen[static_cast<size_t>(r)] == 1, "plan %d: request %d placed %d times", trial, r,
+                                      seen[static_cast<size_t>(r)]);
+    CHECK(a.max_list == maxl, "plan %d: max_list %d vs %d", trial, a.max_list, maxl);
+    const int64_t lds = int64_t(k) * 1024 + 2 * S * nh * (nxec::kEncMd5Step + 16) + S * a.max_list * (k + p + 4) * 8;
+    CHECK(lds <= 160 * 1024, "plan %d: LDS %lld", trial, static_cast<long long>(lds));
+    const int64_t nwg = (G + S - 1) / S;
+    CHECK(static_cast<int64_t>(wg.size()) == nwg, "plan %d: workgroups", trial);
+    for (int64_t b = 0; b < nwg && static_cast<int64_t>(wg.size()) == nwg; b++) {
+      int64_t w = 0;
+      for (int64_t g = b * S; g < std::min(G, (b + 1) * S); g++) w = std::max(w, load[static_cast<size_t>(g)]);
+      CHECK(wg[static_cast<size_t>(b)] == w, "plan %d: workgroup %lld steps", trial, static_cast<long long>(b));
+    }
+    const int64_t smax = std::min<int64_t>(16, 256 / nh);
+    if (R <= int64_t(cus) * smax) CHECK(G == R, "plan %d: %d requests in %lld slots", trial, R, static_cast<long long>(G));
+    if (G == int64_t(cus) * smax && R > G) {  // one wave, lists under the LDS cap: list scheduling bound
+      const int64_t mx = *std::max_element(load.begin(), load.end());
+      bound_checked++;
+      CHECK(mx <= (total + G - 1) / G + longest_req, "plan %d: longest slot %lld, average %lld, longest request %lld",
+            trial, static_cast<long long>(mx), static_cast<long long>(total / G), static_cast<long long>(longest_req));
+    }
+  }
+  std::printf("files slot plans: 300 checked, %d against the list-scheduling bound\n", bound_checked);
+}
+
 int main() {
   gf_and_planning();
+  files_slot_plan();
   argument_validation();
   ini_files();
   std::vector<std::thread> th;
