@@ -246,3 +246,19 @@ def test_host_placed_digests_fail_loudly_without_a_device():
             assert e.value.code == _lib.NXEC_ERR_NODEV
     finally:
         lib.nxec_set_digest_placement(prev)
+
+
+def test_product_build_and_round4_entry_points_without_a_device():
+    """The product build carries no design-probe kernels (make PROBES=1 does),
+    and the round-4 entry points validate before any device use: the kernel
+    timers and every flag combination of the multi-file write refuse a
+    missing context."""
+    assert nxec.design_probes() is False
+    ms, n = ctypes.c_double(-1.0), ctypes.c_int64(-1)
+    assert _lib.lib.nxec_kernel_timing(None, 1) == _lib.NXEC_ERR_INVALID
+    assert _lib.lib.nxec_kernel_time(None, ctypes.byref(ms), ctypes.byref(n)) == _lib.NXEC_ERR_INVALID
+    ln = (ctypes.c_int64 * 1)(100)
+    ptrs = (ctypes.c_void_p * 1)(None)
+    for flags in (0, nxec.OBJECTS_TAIL_INPLACE, nxec.OBJECTS_ASYNC, nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC, 4):
+        assert _lib.lib.nxec_encode_objects_ex(None, 14, 10, 1, ptrs, ln, 1 << 20, None, None, None, flags,
+                                               None) == _lib.NXEC_ERR_INVALID
