@@ -13,11 +13,13 @@ LIBDIR   := nexoedge_amd/lib
 CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj
 
-LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_runtime.hip $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip $(CSRC)/nxec_files_md5.hip \
+LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_context.cpp $(CSRC)/nxec_stripes.cpp $(CSRC)/nxec_objects.cpp \
+            $(CSRC)/nxec_host_paths.cpp $(CSRC)/nxec_host_encode.cpp $(CSRC)/nxec_agent.cpp $(CSRC)/nxec_probes.cpp \
+            $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip $(CSRC)/nxec_files_md5.hip \
             $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_digest_place.cpp $(CSRC)/nxec_numa.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
-HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_device.h $(CSRC)/nxec_em_common.h $(wildcard $(CSRC)/coding/*.hh)
+HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_runtime.h $(CSRC)/nxec_tuning.h $(CSRC)/nxec_device.h $(CSRC)/nxec_em_common.h $(wildcard $(CSRC)/coding/*.hh)
 
 all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test \
      build/stripe_batch_test build/chunk_replay_test

@@ -54,8 +54,10 @@ def parse(argv=None):
     ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true", default=True,
                     help="also time the pinned H2D->encode->D2H pipeline (default on; N=1 headline workload only)")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false")
-    ap.add_argument("--workload", choices=sorted(["rs10_4", "repair12", "mixed16", "write14", "object", "files", "config1"]), default="rs10_4",
-                    help="rs10_4 = headline (configs 2+3); repair12 = config 4; mixed16 = config 5 (one chunk size)")
+    ap.add_argument("--workload", choices=sorted(["rs10_4", "decode_full", "repair12", "mixed16", "write14", "object",
+                                                 "files", "config1"]), default="rs10_4",
+                    help="rs10_4 = headline (configs 2+3); decode_full = config 3 on RSCode::decode's all-k output; "
+                         "repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
     ap.add_argument("--layout", choices=["auto", "natural", "recover"], default="auto",
@@ -206,7 +208,7 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    # round-4 passes on the shipped library (tools/gpu_r04_final.sh; every dispatch
+    # round-4 passes on the shipped library (tools/archive/gpu_r04_final.sh; every dispatch
     # of the roofline kernel labelled with the bench line's bytes per launch);
     # tests/test_bench_line.py checks each file's lib_sha16 against libnxec.so;
     # only the default layout the passes ran with (other layouts report traffic null)
@@ -233,8 +235,9 @@ def load_traffic(args, wl_name, launch_bytes):
     (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, gfx950 x2 read correction): the
     measured traffic/algorithmic ratio of that op's dispatches times this
     launch's algorithmic bytes, with the PMC file and the library hash it was
-    measured on (compare with roofline.lib_sha16: a mismatch means the pass
-    predates the running library).  (None, None) when no pass covers this workload."""
+    measured on and whether that is the running library (`same_library`:
+    false means the pass predates it).  (None, None) when no pass covers this
+    workload."""
     key = PMC_SUMMARIES.get((wl_name, args.chunk, args.layout))
     if key is None:
         return None, None
@@ -250,6 +253,9 @@ def load_traffic(args, wl_name, launch_bytes):
     ratio = sum(d["hbm_bytes"] / d["algorithmic_bytes"] for d in disp) / len(disp)
     src = {"file": "profiles/" + key[0], "lib_sha16": doc.get("lib_sha16"), "dispatches": len(disp),
            "traffic_over_algorithmic": round(ratio, 5)}
+    # a pass on another build still bounds the traffic (the kernels' access
+    # pattern), but the line says so instead of passing it off as this library's
+    src["same_library"] = src["lib_sha16"] == lib_sha16()
     return int(round(ratio * launch_bytes)), src
 
 
@@ -267,6 +273,8 @@ class Workload:
         self.roof_bytes, self.kernel_timer = roof_bytes, kernel_timer
         # erase-and-rebuild checks run after the timed region: [(label, erase(), rebuild())] on buffers[0]
         self.erase = erase or []
+        # checksum buffers[0] must have after the warmup (None: only consistency is checked)
+        self.expect_sum = None
 
 
 def erase_checks(wl, ctx, want):
@@ -329,6 +337,46 @@ def wl_rs10_4(args, ctx, stream, rank):
     # per-kernel mean does
     return Workload("rs10_4", "GiB/s RS(10,4) encode+decode, 1 MiB chunks, device-resident", config, ops, [buf],
                     f"{kern} K={k} rows={p} work-queue (encode + recover launches)", ns, roof_ops=2, erase=erase)
+
+
+def wl_decode_full(args, ctx, stream, rank):
+    """Config 3 on the reference's own read contract: RSCode::decode returns
+    all k data chunks of the stripe (the k x k inverse's rows, rs.cc:114,
+    175-181, 228-230), not only the lost ones.  nxec_rs_decode_stripes reads
+    the k surviving chunks chosen as rs.cc:252-265 does and writes all k data
+    chunks to a separate [stripe][k][cs] output: the erased ones rebuilt,
+    the surviving ones passed through (unit rows of the inverse).  4 erasures,
+    rotating over the headline's three patterns; 2k*cs per stripe."""
+    n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
+    cst, stripe, lay = layout(args, n, cs)
+    buf = nxec.DeviceBuffer(ns * stripe)
+    buf.fill_random(0xDEC0DE + rank * 7919)
+    ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream)
+    out = nxec.DeviceBuffer(ns * k * cs)
+
+    def dec(pat):
+        ctx.rs_decode(n, k, pat, buf.ptr, cst, stripe, out.ptr, cs, k * cs, cs, ns, stream)
+
+    # parity-only loss: every output row is a pass-through of its data chunk,
+    # so the output is the data itself -- the checksum every pattern must give
+    dec(PATTERNS[1])
+    ctx.sync()
+    copy_sum = out.checksum()
+    ops = [("decode_full", lambda i: dec(PATTERNS[i % len(PATTERNS)]), ns * 2 * k * cs)]
+    config = {
+        "workload": f"RS(10,4) (n,k)=({n},{k}) full-output decode (all k data chunks, rs.cc:114,228-230), "
+                    f"4 erasures, {cs >> 10} KiB chunks, {ns}-stripe batch per GPU",
+        "stripes_per_gpu": ns, "chunk_bytes": cs, "erasure_patterns": PATTERNS, "layout": lay,
+        "byte_accounting": "k surviving chunks read + k data chunks written = 2k*cs per stripe",
+        "launch": json.loads(ctx.describe_launch(len(PATTERNS[0]), k, cs, ns)),
+    }
+    kern = config["launch"]["kernel"]
+    erase = [(f"decode{pat}", lambda: out.memset(0), lambda pat=pat: dec(pat)) for pat in PATTERNS]
+    wl = Workload("decode_full", "GiB/s RS(10,4) full-output decode (reference contract), 1 MiB chunks, "
+                  "device-resident", config, ops, [out, buf], f"{kern} K={k} copy-through (full-output decode)", ns,
+                  erase=erase)
+    wl.expect_sum = copy_sum
+    return wl
 
 
 def wl_repair12(args, ctx, stream, rank):
@@ -511,9 +559,9 @@ def wl_files(args, ctx, stream, rank):
     tail_written = sum((cl + 15) // 16 * 16 for (ns, nf, cl), L in zip(layouts, lengths)
                        if ns > nf and (L - nf * k * M) % cl)
     # k_files_md5's own bytes per launch: every request's k data chunks read
-    # (last stripes: the whole ones from the object, the partial and all-zero
-    # ones from their tail slots, written there by the pad copy launched just
-    # before) and p parity chunks written, at the request's chunk length
+    # (last stripes: in place from the object, the chunks past the data from
+    # the zero line) and p parity chunks written, at the request's chunk length;
+    # the kernel also writes each partial chunk to its tail slot (tail_written)
     kernel_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts)
     longest, nreq = files_longest_slot(n, k, M, lengths)
     # NXEC_OBJECTS_ASYNC: the host plans batch i + 1 while batch i codes (the
@@ -540,8 +588,8 @@ def wl_files(args, ctx, stream, rank):
                                           "(profiles/r02_encode_md5_role_probes.log)"}}
     return Workload("files", "GiB/s multi-file write (encode+MD5), RS(10,4), 1 MiB max chunk, device-resident",
                     config, ops, [arena, par, tail, md5],
-                    "k_files_md5<10> (encode_objects_ex(TAIL_INPLACE | ASYNC): after one small k_pad_chunks launch "
-                    "for the last stripes' partial chunks, one k_files_md5 launch codes and hashes every stripe)",
+                    "k_files_md5<10> (encode_objects_ex(TAIL_INPLACE | ASYNC): one launch codes and hashes every "
+                    "stripe, last stripes read in place with their partial chunk masked and stored to the tail arena)",
                     total, roof_bytes=kernel_bytes,
                     kernel_timer=(lambda: ctx.kernel_timing(True), ctx.kernel_time))
 
@@ -632,7 +680,7 @@ def cpu_baseline_config1(args):
     return out
 
 
-WORKLOADS = {"rs10_4": wl_rs10_4, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14,
+WORKLOADS = {"rs10_4": wl_rs10_4, "decode_full": wl_decode_full, "repair12": wl_repair12, "mixed16": wl_mixed16, "write14": wl_write14,
              "object": wl_object, "files": wl_files, "config1": wl_config1}
 
 
@@ -767,7 +815,8 @@ def main():
     elapsed = grp.max(t1 - t0)
     total_bytes = grp.sum(float(step_bytes * args.steps))
     numa_nodes = [int(v) for v in grp.gather(numa_node)]
-    verified = grp.sum(0.0 if wl.buffers[0].checksum() == sum_before else 1.0) == 0.0
+    consistent = wl.buffers[0].checksum() == sum_before and wl.expect_sum in (None, sum_before)
+    verified = grp.sum(0.0 if consistent else 1.0) == 0.0
     # outside the timed region: erase chunks for real and rebuild them
     rebuilt = erase_checks(wl, ctx, sum_before)
     verified = grp.sum(0.0 if verified and all(rebuilt.values()) else 1.0) == 0.0

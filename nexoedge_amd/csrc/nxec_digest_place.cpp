@@ -259,8 +259,7 @@ class DigestHost {
     nthreads_ = std::max(0, std::min(nt, 256));
     cpus_ = cpu_budget();
     if (const char *e = std::getenv("NXEC_DIGEST_CPUS")) cpus_ = std::max(1.0, std::atof(e));
-    host_callers_ = cpus_;
-    if (const char *e = std::getenv("NXEC_DIGEST_HOST_CALLERS")) host_callers_ = std::max(0.0, std::atof(e));
+    host_callers_ = tuning().digest_host_callers > 0 ? tuning().digest_host_callers : cpus_;
     md_ = EVP_MD_fetch(nullptr, "MD5", nullptr);
   }
   ~DigestHost() {

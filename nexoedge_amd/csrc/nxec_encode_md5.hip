@@ -420,8 +420,7 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
                       const void *dst, int64_t dst_stripe_stride, const uint32_t *dst_off, const uint32_t *copy_off) {
   if (k < 1 || k > kEncMd5MaxK || rows < 0 || rows > kMaxRowsPerPass) return false;
   if (len <= 0 || len % kEncMd5Step != 0 || len / kEncMd5Step >= (int64_t(1) << 31)) return false;
-  if (const char *e = std::getenv("NXEC_FUSED_MD5"))
-    if (e[0] == '0') return false;  // A/B: two kernels (coding, then MD5)
+  if (!tuning().fused_md5) return false;  // probe: two kernels (coding, then MD5)
   uint64_t bits = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
                   static_cast<uint64_t>(src_stripe_stride) | static_cast<uint64_t>(dst_stripe_stride);
   for (int j = 0; j < k; j++) bits |= src_off[j];
@@ -484,31 +483,27 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   int64_t S = std::min(kEmMaxStripes, kEmMaxRows / n);  // n: hashed chunks per stripe
   const int64_t per_cu = (a.nstripes + std::max(num_cus, 1) - 1) / std::max(num_cus, 1);
   if (per_cu < S) S = per_cu;
-  if (const char *e = std::getenv("NXEC_EM_S"))  // tuning only: stripes per workgroup
-    S = std::max<int64_t>(1, std::min<int64_t>(std::atoi(e), std::min(kEmMaxStripes, kEmMaxRows / n)));
+  if (tuning().em_stripes > 0)  // probe: stripes per workgroup
+    S = std::max<int64_t>(1, std::min<int64_t>(tuning().em_stripes, std::min(kEmMaxStripes, kEmMaxRows / n)));
   a.stripes_per_group = static_cast<int32_t>(S);
-  a.hash_prio = 0;
-  if (const char *e = std::getenv("NXEC_EM_PRIO")) a.hash_prio = std::atoi(e);
+  a.hash_prio = tuning().em_prio;
   const int64_t grid = (a.nstripes + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
   int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
 #if NXEC_DESIGN_PROBES
-  if (const char *e = std::getenv("NXEC_EM_PROBE"))
-    if (a.k == 10 && a.hash_src) fn = kEmProbe[std::atoi(e) & 7];
+  if (tuning().em_probe >= 0 && a.k == 10 && a.hash_src) fn = kEmProbe[tuning().em_probe & 7];
   // A/B: conflict-free split-nibble tables (k = 10, sources hashed; 40 KiB of tables)
-  if (const char *e = std::getenv("NXEC_EM_TABLES"))
-    if (e[0] == 'n' && a.k == 10 && a.hash_src && 10 * 4096 + 2 * S * n * kEmRow <= kEmLds) {
-      fn = kEmNib;
-      lds = 10 * 4096 + static_cast<int>(2 * S * n * kEmRow);
-    }
+  if (tuning().em_nibble && a.k == 10 && a.hash_src && 10 * 4096 + 2 * S * n * kEmRow <= kEmLds) {
+    fn = kEmNib;
+    lds = 10 * 4096 + static_cast<int>(2 * S * n * kEmRow);
+  }
   // A/B: hash lanes read the source chunks from global memory (only the
   // outputs' rows in LDS; k = 10, sources hashed, full-output copies off)
-  if (const char *e = std::getenv("NXEC_EM_HASHSRC"))
-    if (e[0] == 'g' && a.k == 10 && a.hash_src && a.hash_dst && !a.any_copy && !a.ok) {
-      fn = kEmHg;
-      lds = 10 * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
-    }
+  if (tuning().em_hashsrc_global && a.k == 10 && a.hash_src && a.hash_dst && !a.any_copy && !a.ok) {
+    fn = kEmHg;
+    lds = 10 * 1024 + static_cast<int>(2 * S * a.p * kEmRow);
+  }
 #endif
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), lds,
                      static_cast<hipStream_t>(stream), a);

@@ -20,22 +20,22 @@ namespace nxec {
 
 namespace {
 
-// k_files_md5 reads HBM (a step of ~2 us is many load latencies), and its
-// last-stripe path needs registers of its own: at most 3 steps in flight,
-// 2 from k = 13 (no spills through k = 16); without that path (TAIL = false)
-// up to 4 as k_mul_md5, as the 64-bit source pointers leave room (4 through
-// k = 11, 3 through 14, then 2)
-template <int K, bool TAIL = true>
+// k_files_md5 reads HBM (a step of ~2 us is many load latencies): up to 4
+// steps in flight as k_mul_md5, as the 64-bit source pointers leave room (4
+// through k = 11, 3 through 14, then 2); the masked-chunk state takes one step
+// (3 and 4 steps measured the same in round 4), two from k = 13 (no spills)
+template <int K, bool MASK>
 constexpr int fm_depth() {
-  return !TAIL ? (gm_depth<K>() > 4 ? 4 : gm_depth<K>()) : K >= 13 ? 2 : gm_depth<K>() > 3 ? 3 : gm_depth<K>();
+  constexpr int cap = !MASK ? 4 : K >= 13 ? 2 : 3;
+  return gm_depth<K>() > cap ? cap : gm_depth<K>();
 }
 
 // The multi-file write in one launch (nxec_encode_objects; the per-file
 // loop of Proxy::writeFileStripes, proxy_file_ops.cc:557-666, with
 // writeFileStripe's encode + Chunk::computeMD5 of all n chunks,
 // chunk_manager.cc:66-452): k_mul_md5's code/hash split over pointer tables,
-// every request (a full stripe read in place from its object, or a file's
-// zero-padded last stripe in the tail arena) with its own chunk length.
+// every request (a full stripe, or a file's last stripe, read in place from
+// its object) with its own chunk length.
 //
 // Requests are packed into slots (plan_files_slots): a slot is one stripe's
 // worth of lanes -- 16 code lanes, k + p hash lanes -- that runs its requests
@@ -52,23 +52,33 @@ constexpr int fm_depth() {
 // bytes past the chunk's end masked off) and starts the next chain at once.
 // A lane past its request's end in that request's last step re-reads its
 // last in-bounds vector, stores to scratch and leaves its LDS row alone.
-// PROBE (design probes only, K = 10, NXEC_FM_PROBE; outputs are NOT valid),
-// as k_mul_md5's: bit 0 no MD5 rounds, bit 1 no table lookups, bit 2 no
-// global loads or stores, bit 3 (alone, 8) no tail-arena stores, bit 4
-// (alone, 16) last stripes coded like whole stripes (no tail handling).
-// TAIL = false: no request reads a last stripe from its object (a.tail_src is
-// null: in place, last stripes are ordinary requests) -- every tail branch,
-// its state and its registers compile out of the step loop.  TSTORE (with
-// TAIL = false; a.tail_store): last stripes are in-place requests and the
-// code lanes also store their whole data chunks to the tail arena.
-template <int K, int PROBE = 0, bool TAIL = true, bool TSTORE = false>
+//
+// A last stripe (chunk_manager.cc:390-399) is an ordinary request whose data
+// chunks are read where they lie in the object; the host points the chunks
+// past the data at an all-zero line.  MASK: a request may name one data
+// chunk jm that holds the object's last bytes (vm of them, fewer than the
+// chunk length): the lane's vectors of that chunk are read in place while
+// they lie inside the data, the one vector that straddles the end is read
+// byte by byte (nothing past the object's last byte is touched) and zero
+// padded, and from there on the chunk reads the zero line -- no pad copy
+// before the launch.  Both are rare per-lane events (one wave-uniform test
+// per step), so the step loop keeps the tail-free form.  With store mode 1
+// the code lanes also write that chunk, zero padded, to its tail-arena slot
+// (NXEC_OBJECTS_TAIL_INPLACE: the one chunk of a last stripe the caller
+// sends from the arena).  TSTORE (whole tail arena, no flag): the code lanes
+// store every data chunk j < j0 of a last stripe to its slot, bytes past the
+// chunk's length zeroed.
+// PROBE (design probes only, K = 10; outputs are NOT valid), as k_mul_md5's:
+// bit 0 no MD5 rounds, bit 1 no table lookups, bit 2 no global loads or stores.
+template <int K, int PROBE = 0, bool MASK = false, bool TSTORE = false>
 __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   extern __shared__ __align__(16) uint8_t lds[];
   const int nh = K + a.p;
   const int S = a.slots_per_group;
   const int L = a.max_list;
-  // request record: K sources, p outputs, digest base, length, tail source, tail bytes
-  const int rec = K + a.p + 4;
+  // request record: K sources, p outputs, digest base, length, tail slot,
+  // tail geometry (cls | vm << 32), mask (jm | j0 << 8 | mode << 16)
+  const int rec = K + a.p + 5;
   uint32_t *tab = reinterpret_cast<uint32_t *>(lds);
   uint8_t *buf = lds + K * 1024;
   const uint32_t buf_bytes = static_cast<uint32_t>(S * nh * kEmRow);
@@ -91,14 +101,15 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       else if (f == K + a.p + 1)
         v = static_cast<uint64_t>(a.lens[r]);
       else if (f == K + a.p + 2)
-        v = a.tail_src ? reinterpret_cast<uint64_t>(a.tail_src[r]) : 0;
+        v = a.last_slot ? a.last_slot[r] : 0;
+      else if (f == K + a.p + 3)
+        v = a.last_geom ? a.last_geom[r] : 0;
       else
-        v = a.tail_rem ? static_cast<uint64_t>(a.tail_rem[r]) : 0;
+        v = a.last_mask ? a.last_mask[r] : static_cast<uint64_t>(K | (K << 8));
     }
     rq[i] = v;
   }
   __syncthreads();
-  if (a.wg_clock && threadIdx.x == 0) a.wg_clock[blockIdx.x * 3] = __builtin_amdgcn_s_memrealtime();
   const int nsteps = a.wg_steps[blockIdx.x];
   auto steps_of = [](int64_t len) { return static_cast<int>((len + kEncMd5Step - 1) / kEncMd5Step); };
 
@@ -123,74 +134,44 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     int64_t len0 = len_of(0);
     int lT = steps_of(len0), ltcl = max(tmax_of(len0), 0);
     const uint8_t *sp[K];
-    // a lane whose column holds no byte of the request (chunks under 256
-    // bytes) reads the scratch line: nothing past a chunk's 16-byte padding is read
-    // A last stripe read from its object (tail source != 0): data chunk j is
-    // tail bytes [j*cl, (j+1)*cl), valid below min((j+1)*cl, rem): `tl` = cl
-    // (0 for a full stripe), `jf` = chunks wholly valid, `last` = the valid
-    // bytes of chunk jf (32-bit: cl <= 1 GiB), `end` = the end of the tail's
-    // last 16-byte line (nothing at or past it is read), `zf` = the first
-    // all-zero chunk (read from the zero scratch line, never masked), `jc` =
-    // the first chunk whose 16-byte column vectors can run past `end` (only
-    // chunks jc..zf-1 are clamped when loaded and, in place, shifted / masked
-    // when computed: below jc a vector past the chunk's own end reads the next
-    // chunk's bytes, which only reach parity bytes past cl -- outside the
-    // parity chunk -- and row bytes the hash lanes mask off)
-    auto tail_state = [&](int li, int64_t cl, uint32_t &tl, uint32_t &jf, uint32_t &last, const uint8_t *&end,
-                          uint32_t &jc, uint32_t &zf) {
-      const uint64_t tb = TAIL && act ? q[li * rec + K + a.p + 2] : uint64_t(0);
-      const int64_t rem = TAIL && act ? static_cast<int64_t>(q[li * rec + K + a.p + 3]) : int64_t(0);
-      const int64_t f = tb && cl > 0 ? min(rem / cl, static_cast<int64_t>(K)) : 0;
-      tl = tb ? static_cast<uint32_t>(cl) : 0u;
-      jf = static_cast<uint32_t>(f);
-      last = f < K && tb ? static_cast<uint32_t>(rem - f * cl) : 0u;
-      end = reinterpret_cast<const uint8_t *>((tb + static_cast<uint64_t>(rem) + 15) & ~uint64_t(15));
-      const int64_t cls = (cl + 15) / 16 * 16;
-      zf = tb ? static_cast<uint32_t>(f < K ? f + (last ? 1 : 0) : K) : static_cast<uint32_t>(K);
-      jc = tb ? static_cast<uint32_t>(rem >= cls && cl > 0 ? min((rem - cls) / cl + 1, static_cast<int64_t>(K)) : 0)
-              : static_cast<uint32_t>(K);
-    };
-    auto valid_of = [](int j, uint32_t tl, uint32_t jf, uint32_t last) {
-      return static_cast<int32_t>(static_cast<uint32_t>(j) < jf ? tl : static_cast<uint32_t>(j) == jf ? last : 0u);
-    };
-    // source pointers of the lane's column: a full stripe's chunks, a tail's
-    // object bytes (at any byte), or -- a lane whose column holds no byte of
-    // the request (chunks under 256 bytes) -- the scratch line: nothing past a
-    // chunk's 16-byte padding is read
+    // MASK: the load cursor's masked chunk (K: none) and its bytes in the object
+    int lj = K;
+    int32_t lvm = 0;
+    // a straddling vector read byte by byte, for the compute step sv_step
+    u32x4 sv = u32x4{0u, 0u, 0u, 0u};
+    int sv_step = -1, sv_j = K;
+    int lsteps = 0;  // load() calls so far: the workgroup step the next load feeds
+    // source pointers of the lane's column: a request's chunks, or -- a lane
+    // whose column holds no byte of the request (chunks under 256 bytes) --
+    // the scratch line: nothing past a chunk's 16-byte padding is read
     auto set_src = [&](int li, bool has) {
-      const uint64_t tb = TAIL && act ? q[li * rec + K + a.p + 2] : uint64_t(0);
-      const int64_t cl = len_of(li);
 #pragma unroll
       for (int j = 0; j < K; j++)
-        sp[j] = act && has ? (tb ? reinterpret_cast<const uint8_t *>(tb) + j * cl
-                                 : reinterpret_cast<const uint8_t *>(q[li * rec + j])) + v * 16
-                           : a.scratch + v * 16;
+        sp[j] = act && has ? reinterpret_cast<const uint8_t *>(q[li * rec + j]) + v * 16 : a.scratch + v * 16;
+      if (MASK) {
+        lj = act && has ? static_cast<int>(q[li * rec + K + a.p + 4] & 0xff) : K;
+        lvm = static_cast<int32_t>(q[li * rec + K + a.p + 3] >> 32);
+      }
     };
     set_src(0, tmax_of(len0) >= 0);
-    uint32_t ltl, ljf, llast, ljc, lzf;
-    const uint8_t *lend;
-    tail_state(0, len0, ltl, ljf, llast, lend, ljc, lzf);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
-      const bool wtl = TAIL && !(PROBE & 16) && __builtin_amdgcn_ballot_w64(ltl != 0) != 0;  // wave-uniform: skip in full-stripe waves
+      // MASK events of this lane's vector of chunk lj: it straddles the
+      // object's end (st), or lies past it / repeats a step (zr: from now on
+      // the chunk reads the zero line)
+      bool st = false, zr = false;
+      if (MASK) {
+        const int32_t co = static_cast<int32_t>(off) + v * 16;
+        st = lj < K && co < lvm && co + 16 > lvm && lt <= ltcl;
+        zr = lj < K && (co >= lvm || lt > ltcl);
+      }
+      const bool wev = MASK && __builtin_amdgcn_ballot_w64(st || zr) != 0;  // wave-uniform
 #pragma unroll
       for (int j = 0; j < K; j++) {
-        // a tail chunk's 16 bytes are read where they lie (global loads take
-        // any byte address), except where they would run past the tail's
-        // last 16-byte line: that lane reads the aligned line holding its
-        // first byte (the compute step shifts it into place), or the scratch
-        // line once nothing of the tail is left
         const uint8_t *pj = sp[j] + off;
-        if (wtl && ltl && static_cast<uint32_t>(j) >= ljc) {  // the few chunks that reach the tail's end
-          if (static_cast<uint32_t>(j) >= lzf)
-            pj = a.scratch + v * 16;  // all zero
-          else
-            pj = pj + 16 <= lend ? pj
-                 : pj < lend     ? reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(pj) & ~uintptr_t(15))
-                                 : a.scratch + v * 16;
-        }
+        if (wev && (st || zr) && j == lj) pj = a.zero + v * 16 + off;
         // plain (cached) loads: a chunk that is not 128-byte aligned (an
-        // object at any 16-byte offset, a tail at any byte) shares its
+        // object at any 16-byte offset, a last stripe at any byte) shares its
         // boundary lines between consecutive steps; streaming loads fetched
         // them once per step
         if (PROBE & 4)  // no HBM traffic: a value the compiler cannot fold
@@ -201,6 +182,27 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         else
           d[j] = dev::ld_global_stream(pj);
       }
+      if (wev) {
+        if (st) {  // the valid bytes only, zero padded (the reference's padding, chunk_manager.cc:390-399)
+          const uint8_t *pb = nullptr;
+#pragma unroll
+          for (int j = 0; j < K; j++)
+            if (j == lj) pb = sp[j] + off;
+          const int nb = lvm - (static_cast<int32_t>(off) + v * 16);
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          for (int b = 0; b < nb; b++) w[b >> 2] |= static_cast<uint32_t>(pb[b]) << (8 * (b & 3));
+          sv = u32x4{w[0], w[1], w[2], w[3]};
+          sv_step = lsteps;
+          sv_j = lj;
+        }
+        if (zr) {
+#pragma unroll
+          for (int j = 0; j < K; j++)
+            if (j == lj) sp[j] = a.zero + v * 16;
+          lj = K;
+        }
+      }
+      lsteps++;
       if (++lt == lT) {
         if (lr + 1 < cnt) {  // next request of the slot (pointers from the LDS table)
           lr++;
@@ -209,21 +211,16 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           lT = steps_of(ln);
           ltcl = max(tmax_of(ln), 0);
           set_src(lr, tmax_of(ln) >= 0);
-          tail_state(lr, ln, ltl, ljf, llast, lend, ljc, lzf);
-        } else {
-          lt = lT - 1;  // past the slot's end: re-read the last step
+        } else {  // past the slot's end: re-read the scratch line
+          lt = lT - 1;
+          ltcl = 0;
+          set_src(lr, false);
         }
       }
     };
     // compute cursor
     int cr = 0, ct = 0, cT = lT, ctmax = act ? tmax_of(len0) : -1;
     bool live = act;
-    uint32_t ctl = ltl, cjf = ljf, clast = llast, cjc = ljc, czf = lzf;
-    const uint8_t *cend = lend;
-    // the tail source and the tail arena's chunk 0 (chunk j at + j*cls), kept
-    // in registers: no per-step read of the request table
-    const uint8_t *ctb = TAIL && act ? reinterpret_cast<const uint8_t *>(q[K + a.p + 2]) : nullptr;
-    uint8_t *ctd = TAIL && act ? reinterpret_cast<uint8_t *>(q[0]) : nullptr;
     uint8_t *dp[kMaxRowsPerPass];
     auto set_dst = [&](int li) {
 #pragma unroll
@@ -231,65 +228,31 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         dp[r] = act && r < a.p ? reinterpret_cast<uint8_t *>(q[li * rec + K + r]) + v * 16 : a.scratch;
     };
     set_dst(0);
-    // a tail chunk's 16 bytes at column v of step ct, at the chunk's valid end
-    // (the lane's bytes run past it): a lane whose load was the aligned line
-    // holding its first byte shifts that line into place, then every byte
-    // from the valid end on is zeroed (the reference's zero padding)
-    auto tail_end = [&](int j, u32x4 x, int32_t nv) {
-      const int32_t pos = ct * kEncMd5Step + v * 16;
-      const uint8_t *addr = ctb + static_cast<int64_t>(j) * ctl + pos;
-      if (addr + 16 > cend) {
-        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(addr)) & 15u, qd = sh >> 2, rb = sh & 3u;
-        const uint32_t w[8] = {x.x, x.y, x.z, x.w, 0u, 0u, 0u, 0u};
-        uint32_t o[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const uint32_t lo = (qd & 2u) ? ((qd & 1u) ? w[i + 3] : w[i + 2]) : ((qd & 1u) ? w[i + 1] : w[i]);
-          const uint32_t up = (qd & 2u) ? ((qd & 1u) ? w[i + 4] : w[i + 3]) : ((qd & 1u) ? w[i + 2] : w[i + 1]);
-          o[i] = __builtin_amdgcn_alignbyte(up, lo, rb);
-        }
-        x = u32x4{o[0], o[1], o[2], o[3]};
-      }
-      const int32_t n = max(nv, 0);
-      uint32_t m[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int keep = n - 4 * i;
-        m[i] = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
-      }
-      return u32x4{x.x & m[0], x.y & m[1], x.z & m[2], x.w & m[3]};
-    };
     uint8_t *row = buf + ls * nh * kEmRow + v * 16;
-    // TSTORE: the compute request's tail slot 0 (nullptr: a full stripe), slot
-    // stride, whole chunks stored (j < sj0) and its chunk length
+    // tail-arena stores of the compute request: slot of its chunk 0 (nullptr:
+    // none), chunk stride, chunks stored whole (TSTORE: j < sj0), the chunk
+    // stored zero padded (mode 1: sjm), chunk length
     uint8_t *std_ = nullptr;
     int64_t scls = 0;
-    int32_t sj0 = 0, scl = 0;
+    int32_t sj0 = 0, sjm = -1, scl = 0;
     auto set_store = [&](int li) {
-      if (!TSTORE) return;
+      if (!TSTORE && !MASK) return;
       std_ = act ? reinterpret_cast<uint8_t *>(q[li * rec + K + a.p + 2]) : nullptr;
-      const uint64_t w = act ? q[li * rec + K + a.p + 3] : 0;
-      scls = static_cast<int64_t>(w & ((uint64_t(1) << 40) - 1));
-      sj0 = static_cast<int32_t>(w >> 40);
+      scls = static_cast<int64_t>(q[li * rec + K + a.p + 3] & 0xffffffffu);
+      const uint64_t m = q[li * rec + K + a.p + 4];
+      sj0 = static_cast<int32_t>((m >> 8) & 0xff);
+      sjm = (m >> 16) & 1 ? static_cast<int32_t>(m & 0xff) : -1;
       scl = static_cast<int32_t>(len_of(li));
     };
     set_store(0);
     auto run = [&](int step, const u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
-      // wave-uniform: only waves holding a last stripe store
+      // wave-uniform: only waves holding a last stripe store, only steps with a straddling vector patch
       const bool wst = TSTORE && __builtin_amdgcn_ballot_w64(ok && std_ != nullptr) != 0;
-      const bool tl = live && ctl != 0;
-      const bool wtc = TAIL && !(PROBE & 16) && __builtin_amdgcn_ballot_w64(tl) != 0;  // wave-uniform: skip in full-stripe waves
-      if (wtc) {
-        // wait for this step's loads here, in uniform control flow: a first
-        // use inside the per-lane tail branches below would be counted
-        // conservatively (vmcnt(0)) and drain the loads of the steps ahead
-#pragma unroll
-        for (int j = 0; j < K; j++) asm volatile("" ::"v"(d[j].x), "v"(d[j].y), "v"(d[j].z), "v"(d[j].w));
-      }
+      const bool hit = MASK && sv_step == step;
+      const bool wsv = MASK && __builtin_amdgcn_ballot_w64(hit) != 0;
       uint8_t *rb = row + (step & 1) * buf_bytes;
       const int32_t pos = ct * kEncMd5Step + v * 16;
-      const int64_t cls = (static_cast<int64_t>(ctl) + 15) / 16 * 16;
       uint32_t acc[16];
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = 0;
@@ -297,27 +260,15 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int j = 0; j < K; j += 2) {
         const int j1 = j + 1 < K ? j + 1 : j;
         u32x4 x0 = d[j], x1 = d[j1];
-        if (wtc && tl) {
-          const int32_t nv0 = valid_of(j, ctl, cjf, clast) - pos, nv1 = valid_of(j1, ctl, cjf, clast) - pos;
-          // shift / mask only where it matters: chunks jc..zf-1 (zero chunks
-          // were read as zeros); in copy mode also every chunk's last vector,
-          // whose bytes past cl go to the tail arena and must be zero
-          const bool m0 = static_cast<uint32_t>(j) < czf && (static_cast<uint32_t>(j) >= cjc || !a.tail_partial_only);
-          const bool m1 = static_cast<uint32_t>(j1) < czf && (static_cast<uint32_t>(j1) >= cjc || !a.tail_partial_only);
-          if (nv0 < 16 && m0) x0 = tail_end(j, x0, nv0);
-          if (nv1 < 16 && m1) x1 = tail_end(j1, x1, nv1);
-          if (ok) {  // the zero-padded data chunks into the tail arena (in place: only the partial one)
-            const bool part0 = j == static_cast<int>(cjf) && clast != 0, part1 = j1 == static_cast<int>(cjf) && clast != 0;
-            if (!(PROBE & 12) && (!a.tail_partial_only || part0)) dev::st_global_stream(ctd + j * cls + pos, x0);
-            if (!(PROBE & 12) && j + 1 < K && (!a.tail_partial_only || part1))
-              dev::st_global_stream(ctd + j1 * cls + pos, x1);
-          }
+        if (wsv) {  // the straddling vector was loaded as zeros: put its bytes in
+          if (hit && sv_j == j) x0 = sv;
+          if (hit && sv_j == j1) x1 = sv;
         }
         if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
           *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = x0;
           if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = x1;
         }
-        if (wst && ok && std_) {  // whole chunks to the tail arena, zero past the chunk's end
+        if (wst && ok && std_) {  // data chunks to the tail arena, zero past the chunk's end
           const int32_t nv = scl - pos;
           uint32_t m[4];
 #pragma unroll
@@ -338,6 +289,10 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
 #pragma unroll
         for (int i = 0; i < 16; i++) asm volatile("" : "+v"(acc[i]));
       }
+      // mode 1: the masked chunk, zero padded, to its slot (read back from this
+      // lane's own LDS row: LDS accesses of one wave complete in order)
+      if (MASK && __builtin_amdgcn_ballot_w64(ok && sjm >= 0) != 0 && ok && sjm >= 0)
+        dev::st_global_stream(std_ + sjm * scls + pos, *reinterpret_cast<const u32x4 *>(rb + sjm * kEmRow));
       uint32_t o[4][4];
       rows_of(acc, o);
       const int64_t off = static_cast<int64_t>(ct) * kEncMd5Step;
@@ -358,18 +313,13 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
           cT = steps_of(ln);
           ctmax = tmax_of(ln);
           set_dst(cr);
-          tail_state(cr, ln, ctl, cjf, clast, cend, cjc, czf);
-          if (TAIL) {
-            ctb = reinterpret_cast<const uint8_t *>(q[cr * rec + K + a.p + 2]);
-            ctd = reinterpret_cast<uint8_t *>(q[cr * rec]);
-          }
           set_store(cr);
         } else {
           live = false;
         }
       }
     };
-    constexpr int D = fm_depth<K, TAIL>();
+    constexpr int D = fm_depth<K, MASK>();
     u32x4 ring[D][K];
 #pragma unroll
     for (int j = 0; j < D - 1; j++) load(ring[j]);
@@ -390,7 +340,6 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         run(step + j, ring[j]);
       }
     }
-    if (a.wg_clock && threadIdx.x == 0) a.wg_clock[blockIdx.x * 3 + 1] = __builtin_amdgcn_s_memrealtime();
     return;
   }
 
@@ -493,33 +442,19 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
   } else {
     proc(m0);
   }
-  if (a.wg_clock && threadIdx.x == kEmCodeLanes) a.wg_clock[blockIdx.x * 3 + 2] = __builtin_amdgcn_s_memrealtime();
 }
 
 using FmKernel = void (*)(const FilesMd5Args);
-template <int... Ks>
+template <bool MASK, bool TSTORE, int... Ks>
 constexpr std::array<FmKernel, sizeof...(Ks)> fm_table(std::integer_sequence<int, Ks...>) {
-  return {{&k_files_md5<Ks + 1>...}};
+  return {{&k_files_md5<Ks + 1, 0, MASK, TSTORE>...}};
 }
-const std::array<FmKernel, kFilesMd5MaxK> kFm = fm_table(std::make_integer_sequence<int, kFilesMd5MaxK>{});
-template <int... Ks>
-constexpr std::array<FmKernel, sizeof...(Ks)> fm_table_nt(std::integer_sequence<int, Ks...>) {
-  return {{&k_files_md5<Ks + 1, 0, false>...}};
-}
-// no request with a tail source (in place): the tail-free step loop
-const std::array<FmKernel, kFilesMd5MaxK> kFmNt = fm_table_nt(std::make_integer_sequence<int, kFilesMd5MaxK>{});
-template <int... Ks>
-constexpr std::array<FmKernel, sizeof...(Ks)> fm_table_st(std::integer_sequence<int, Ks...>) {
-  return {{&k_files_md5<Ks + 1, 0, false, true>...}};
-}
-// in-place requests that also store last stripes' whole chunks to the tail arena
-const std::array<FmKernel, kFilesMd5MaxK> kFmSt = fm_table_st(std::make_integer_sequence<int, kFilesMd5MaxK>{});
+// [plain / masked chunks / masked chunks + whole tail arena][k - 1]
+const std::array<FmKernel, kFilesMd5MaxK> kFm[3] = {
+    fm_table<false, false>(std::make_integer_sequence<int, kFilesMd5MaxK>{}),
+    fm_table<true, false>(std::make_integer_sequence<int, kFilesMd5MaxK>{}),
+    fm_table<true, true>(std::make_integer_sequence<int, kFilesMd5MaxK>{})};
 #if NXEC_DESIGN_PROBES
-// bit 3 alone: no tail-arena stores (everything else as the product);
-// bit 4 alone: last stripes read straight from the object like whole
-// stripes, no clamps, masks or tail stores (timing only)
-const FmKernel kFmProbe8 = &k_files_md5<10, 8>;
-const FmKernel kFmProbe16 = &k_files_md5<10, 16>;
 const FmKernel kFmProbe[8] = {&k_files_md5<10, 0>, &k_files_md5<10, 1>, &k_files_md5<10, 2>, &k_files_md5<10, 3>,
                               &k_files_md5<10, 4>, &k_files_md5<10, 5>, &k_files_md5<10, 6>, &k_files_md5<10, 7>};
 #endif
@@ -527,10 +462,8 @@ const FmKernel kFmProbe[8] = {&k_files_md5<10, 0>, &k_files_md5<10, 1>, &k_files
 }  // namespace
 
 int prepare_files_md5() {
-  std::vector<FmKernel> fms(kFm.begin(), kFm.end());
-  fms.insert(fms.end(), kFmNt.begin(), kFmNt.end());
-  fms.insert(fms.end(), kFmSt.begin(), kFmSt.end());
-  for (FmKernel fn : fms) {
+  for (int t = 0; t < 3 * kFilesMd5MaxK; t++) {
+    const FmKernel fn = kFm[t / kFilesMd5MaxK][t % kFilesMd5MaxK];
     hipFuncAttributes fa{};
     if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(fn)) != hipSuccess || fa.sharedSizeBytes != 0)
       return set_error(NXEC_ERR_HIP, "k_files_md5: static LDS present (the tables must start at LDS byte 0)");
@@ -538,8 +471,7 @@ int prepare_files_md5() {
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5): %s", hipGetErrorString(e));
   }
 #if NXEC_DESIGN_PROBES
-  for (FmKernel fn : {kFmProbe[0], kFmProbe[1], kFmProbe[2], kFmProbe[3], kFmProbe[4], kFmProbe[5], kFmProbe[6],
-                      kFmProbe[7], kFmProbe8, kFmProbe16}) {
+  for (FmKernel fn : kFmProbe) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, kEmLds);
     if (e != hipSuccess) return set_error(NXEC_ERR_HIP, "hipFuncSetAttribute(k_files_md5 probe): %s", hipGetErrorString(e));
   }
@@ -553,8 +485,7 @@ void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cu
   const int64_t R = static_cast<int64_t>(lens.size());
   const int64_t Smax = std::min(kEmMaxStripes, kEmMaxRows / nh);
   const int64_t cus = std::max(num_cus, 1);
-  const char *pe = std::getenv("NXEC_FILES_PACK");
-  const bool pack = !(pe && pe[0] == '0');
+  const bool pack = tuning().files_pack;
   auto steps = [](int64_t len) { return (len + kEncMd5Step - 1) / kEncMd5Step; };
   // at most one workgroup per CU (its LDS), so 256 x Smax slots in one wave:
   // fewer requests than that get a slot each, spread over every CU first
@@ -568,7 +499,7 @@ void plan_files_slots(const std::vector<int64_t> &lens, int k, int p, int num_cu
   }
   S = std::max<int64_t>(S, 1);
   const int64_t lds_free = kEmLds - int64_t(k) * 1024 - 2 * S * nh * kEmRow;
-  const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 4) * 8));
+  const int64_t Lmax = std::max<int64_t>(1, lds_free / (S * (k + p + 5) * 8));
   // slot of every request; loads and list lengths per slot
   std::vector<int32_t> slot_of(static_cast<size_t>(R));
   std::vector<int64_t> load(static_cast<size_t>(G), 0);
@@ -641,8 +572,8 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
       in.slots_per_group < 1 || in.max_list < 1)
     return set_error(NXEC_ERR_INVALID, "files+md5: unsupported arguments");
   FilesMd5Args a = in;
-  a.cached_loads = 1;  // FETCH x2 60.0 -> 43.6 GB per 4096-file batch (= the data bytes), same time
-  if (const char *e = std::getenv("NXEC_FILES_LOADS")) a.cached_loads = e[0] != '0';
+  // cached loads: FETCH x2 60.0 -> 43.6 GB per 4096-file batch (= the data bytes), same time
+  a.cached_loads = tuning().files_cached_loads ? 1 : 0;
   (void)num_cus;
   const int nh = a.k + a.p;
   const int64_t S = a.slots_per_group;
@@ -650,14 +581,13 @@ int launch_files_md5(const FilesMd5Args &in, int num_cus, void *stream) {
     return set_error(NXEC_ERR_INVALID, "files+md5: %lld slots of %d chunks per workgroup", static_cast<long long>(S), nh);
   const int64_t grid = (a.nslots + S - 1) / S;
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "files+md5: batch too large for one launch");
-  const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 4) * 8;
+  const int64_t lds = int64_t(a.k) * 1024 + 2 * S * nh * kEmRow + S * a.max_list * (a.k + a.p + 5) * 8;
   if (lds > kEmLds) return set_error(NXEC_ERR_INVALID, "files+md5: request table does not fit the LDS");
-  FmKernel fn = a.tail_store ? kFmSt[a.k - 1] : a.tail_src ? kFm[a.k - 1] : kFmNt[a.k - 1];
-  if (a.tail_store && (!a.tail_src || !a.tail_rem)) return set_error(NXEC_ERR_INVALID, "files+md5: tail-store tables");
+  if ((a.mask || a.tail_store) && (!a.last_slot || !a.last_geom || !a.last_mask || !a.zero))
+    return set_error(NXEC_ERR_INVALID, "files+md5: last-stripe tables");
+  FmKernel fn = kFm[a.tail_store ? 2 : a.mask ? 1 : 0][a.k - 1];
 #if NXEC_DESIGN_PROBES
-  if (const char *e = std::getenv("NXEC_FM_PROBE"))
-    if (a.k == 10)
-      fn = std::atoi(e) == 8 ? kFmProbe8 : std::atoi(e) == 16 ? kFmProbe16 : kFmProbe[std::atoi(e) & 7];
+  if (tuning().fm_probe >= 0 && a.k == 10 && !a.mask && !a.tail_store) fn = kFmProbe[tuning().fm_probe & 7];
 #endif
   hipLaunchKernelGGL(fn, dim3(static_cast<unsigned>(grid)), dim3(kEmBlock), static_cast<unsigned>(lds),
                      static_cast<hipStream_t>(stream), a);

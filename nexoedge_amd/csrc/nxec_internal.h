@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "nxec.h"
+#include "nxec_tuning.h"
 
 namespace nxec {
 
@@ -233,10 +234,10 @@ int launch_gather_md5(const GatherMd5Args &a, int num_cus, void *stream);
 // k sources src_ptrs[s*k + j] into p outputs dst_ptrs[s*p + r] and hashes
 // all k + p chunks, lens[s] bytes each, digest of chunk c (sources first) at
 // dig_ptrs[s] + c*16.  Bytes up to the next multiple of 16 past lens[s] are
-// readable; outputs are written up to that multiple.  A last stripe
-// (tail_src[s] set) reads its sources from the object instead and writes
-// them zero-padded to src_ptrs.  Every pointer 16-byte aligned (digests and
-// tail_src any); tables in device memory.
+// readable (except in a masked chunk, below); outputs are written up to that
+// multiple.  Source pointers may be at any byte address (the objects' last
+// stripes), outputs and tail slots 16-byte aligned, digests any; tables in
+// device memory.
 //
 // Requests are packed into slots (one stripe's worth of code and hash lanes
 // of a workgroup): slot g runs requests slot_reqs[slot_first[g] ..
@@ -261,29 +262,26 @@ struct FilesMd5Args {
   int32_t k, p;
   int32_t slots_per_group;
   int32_t max_list;           // longest slot list (LDS request table rows per slot)
-  int32_t cached_loads;       // plain loads (default); NXEC_FILES_LOADS=0 streaming (A/B)
+  int32_t cached_loads;       // plain loads (default); streaming with the loads probe
   uint8_t coef[kMaxRowsPerPass * (NXEC_MAX_K + 1)];  // p x k, row-major
-  // A file's last stripe read straight from its object (no pad copy):
-  // tail_src[s] = the object's bytes past its full stripes (any alignment;
-  // nullptr for a full stripe), tail_rem[s] = how many.  Data chunk j of
-  // such a stripe is object bytes [j*lens[s], (j+1)*lens[s]) zero-padded;
-  // the kernel codes and hashes it and also writes it, so padded up to the
-  // next multiple of 16, to src_ptrs[s*k + j] (the tail arena).
-  const uint8_t *const *tail_src;
-  const int64_t *tail_rem;
-  // NXEC_OBJECTS_TAIL_INPLACE: of a last stripe's data chunks only the
-  // partial one (zero-padded) is written to the tail arena; the whole ones
-  // stay where they are in the object, the all-zero ones are not written
-  int32_t tail_partial_only;
-  // Whole tail arena with last stripes as in-place requests (no flag): the
-  // code lanes also store a last stripe's whole data chunks j < j0 -- read in
-  // place from the object -- to their tail slots, bytes past the chunk's
-  // length zeroed.  tail_src[s] = the tail arena's chunk 0 of request s
-  // (nullptr: a full stripe), tail_rem[s] = cls | j0 << 40
+  // Last stripes (null tables: none).  Per request s:
+  //   last_slot[s]  the tail-arena slot of its data chunk 0 (0: nothing stored)
+  //   last_geom[s]  cls | vm << 32: the slots' chunk stride, and the bytes of
+  //                 the masked chunk that lie in the object
+  //   last_mask[s]  jm | j0 << 8 | mode << 16: the masked data chunk (k:
+  //                 none) -- read in place below vm, zero padded from vm, the
+  //                 vector across vm read byte by byte --, the chunks a
+  //                 whole-tail-arena call stores (j < j0), mode 1: store the
+  //                 masked chunk zero padded to its slot
+  const uint64_t *last_slot;
+  const uint64_t *last_geom;
+  const uint32_t *last_mask;
+  const uint8_t *zero;  // >= max(lens) + 16 zero bytes: data chunks past a last stripe's data
+  int32_t mask;         // some request has a masked chunk
+  // Whole tail arena (no NXEC_OBJECTS_TAIL_INPLACE): the code lanes store a
+  // last stripe's data chunks j < j0 to their slots, bytes past the chunk's
+  // length zeroed
   int32_t tail_store;
-  // NXEC_FILES_CLOCK=1 (diagnostics): per workgroup, s_memrealtime at the
-  // start, at the end of code wave 0 and at the end of hash wave 0
-  unsigned long long *wg_clock;
 };
 // Slot plan for `lens` (descending): fills slot_first / slot_reqs / wg_steps
 // and the args' nslots / slots_per_group / max_list.  NXEC_FILES_PACK=0 gives

@@ -773,11 +773,10 @@ int hip_fail(hipError_t e, const char *what) {
   return set_error(NXEC_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-// LDS replication policy (NXEC_LDS_R=1|8|16 overrides, for tuning only).
+// LDS replication policy (the LDS-replication probe overrides it, nxec_tuning.h).
 int choose_r(int k, bool tunable) {
   if (k > kMaxTemplK) return 1;
-  const char *env = tunable ? std::getenv("NXEC_LDS_R") : nullptr;
-  const int want = env ? std::atoi(env) : 0;
+  const int want = tunable ? tuning().lds_r : 0;
   if (want == 1) return 1;
   if (want == 8) return 8;
   if (want == 16 && k <= 10) return 16;
@@ -803,12 +802,11 @@ int table_lds(int k, int r) {
 
 }  // namespace
 
-// single-row passes use the VALU nibble-table kernel (NXEC_ALGO=lds forces LDS, for A/B)
+// single-row passes use the VALU nibble-table kernel (a probe forces LDS tables, nxec_tuning.h)
 bool use_perm(int k, int rows, bool full, bool copy, bool gather) {
   if (rows != 1 || k > kPermMaxK || !full || copy) return false;
   if (k == 11 && !gather) return false;  // this instantiation alone spills (hipcc 7.2 schedule); LDS tables instead
-  const char *env = std::getenv("NXEC_ALGO");
-  return !(env && std::strcmp(env, "lds") == 0);
+  return !tuning().lds_single_row;
 }
 
 LaunchInfo plan_launch(int k, int rows, int64_t vec_count, int64_t nstripes, int num_cus, bool full, bool copy,
@@ -911,11 +909,6 @@ int launch_failed(hipError_t e, const char *what, int slot, hipStream_t st) {
   return rc;
 }
 
-// NXEC_TILE_ORDER=static: static tile runs instead of the work queue (A/B probes only)
-bool static_order() {
-  const char *env = std::getenv("NXEC_TILE_ORDER");
-  return env && std::strcmp(env, "static") == 0;
-}
 
 int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -932,7 +925,7 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
     for (int pi = 0; pi < 2; pi++) {
       if (parts[pi][1] <= 0) continue;
       MulArgs b = a;
-      b.queue_slot = static_order() ? -1 : static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
+      b.queue_slot = tuning().static_order ? -1 : static_cast<int32_t>(g_next_slot.fetch_add(1, std::memory_order_relaxed) % kQueueSlots);
       b.tiles_per_grab = tiles_per_grab(b);
       // chunks of >= 2 MiB at a power-of-two-aligned chunk stride: walk groups
       // of 8 stripes column-major, so the in-flight window spans 8 stripes
@@ -942,7 +935,7 @@ int launch_mul(const MulArgs &a, bool vec_ok, int num_cus, void *stream) {
       // (4 MiB + 2 KiB: 0.758 at sg 1, profiles/r02_layout_sweep.log).
       const bool aliased = a.src_ptrs != nullptr || a.src_chunk_stride % (int64_t(1) << 20) == 0;
       b.stripe_group = ((b.vec_count + kBlock - 1) / kBlock >= 128 && aliased) ? 8 : 1;
-      if (const char *e = std::getenv("NXEC_STRIPE_GROUP")) b.stripe_group = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+      if (tuning().stripe_group > 0) b.stripe_group = static_cast<uint32_t>(tuning().stripe_group);
       b.vec_begin = a.vec_begin + parts[pi][0];
       b.vec_count = parts[pi][1];
       const bool is_full = pi == 0;

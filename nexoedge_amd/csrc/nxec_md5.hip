@@ -272,8 +272,8 @@ Md5Kernel pick_nt(bool nt) {
 
 Md5Kernel md5_kernel() {
   static const Md5Kernel k = [] {
-    int d = 2, g = 8, nt = 0;
-    if (const char *e = getenv("NXEC_MD5_CFG")) sscanf(e, "%d,%d,%d", &d, &g, &nt);
+    const int d = tuning().md5_depth, g = tuning().md5_group;  // the ring-shape probe (nxec_tuning.h)
+    const bool nt = tuning().md5_nt;
     if (d == 2 && g == 1) return pick_nt<2, 1>(nt);
     if (d == 4 && g == 1) return pick_nt<4, 1>(nt);
     if (d == 2 && g == 2) return pick_nt<2, 2>(nt);

@@ -262,3 +262,37 @@ def test_product_build_and_round4_entry_points_without_a_device():
     for flags in (0, nxec.OBJECTS_TAIL_INPLACE, nxec.OBJECTS_ASYNC, nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC, 4):
         assert _lib.lib.nxec_encode_objects_ex(None, 14, 10, 1, ptrs, ln, 1 << 20, None, None, None, flags,
                                                None) == _lib.NXEC_ERR_INVALID
+
+
+DEPLOYMENT_SETTINGS = {"NXEC_HOST_THREADS", "NXEC_HOST_DIRECT", "NXEC_SLOT_POOL_MAX", "NXEC_HOST_ARENA_MAX",
+                       "NXEC_CHUNK_ARENA_MIN", "NXEC_CHUNK_MD5", "NXEC_DIGEST_PLACE", "NXEC_DIGEST_THREADS",
+                       "NXEC_DIGEST_CPUS"}
+TEST_HOOKS = {"NXEC_TEST_FAULT", "NXEC_SYSFS_ROOT"}
+
+
+def test_product_library_reads_only_the_documented_settings():
+    """The default libnxec.so names no environment variable but the deployment
+    settings INTEGRATION.md lists (each with its default) and the two test
+    hooks, and carries no design-probe kernel: the A/B knobs and their
+    kernels exist only in a `make PROBES=1` build (nxec_tuning.h)."""
+    import re
+    import subprocess
+    if nxec.design_probes():
+        pytest.skip("design-probe build")
+    blob = open(_lib.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"NXEC_[A-Z][A-Z0-9_]+", blob))
+    env_like = {n.decode() for n in names if not n.startswith((b"NXEC_ERR", b"NXEC_OK"))}
+    assert env_like == DEPLOYMENT_SETTINGS | TEST_HOOKS, env_like ^ (DEPLOYMENT_SETTINGS | TEST_HOOKS)
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    table = doc[doc.index("## Deployment settings"):]
+    for name in DEPLOYMENT_SETTINGS:
+        assert re.search(r"^\| `" + name + r"` \| [^|]+ \|", table, re.M), name
+    # probe kernels: k_mul_md5<K, HSRC, PROBE, NIBBLE, HASHSRC_GLOBAL> with a probe
+    # or variant argument set, k_files_md5<K, PROBE != 0, ...>
+    syms = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    em = re.findall(rb"k_mul_md5ILi(\d+)ELb([01])ELi(\d+)ELb([01])ELb([01])E", blob)
+    fm = re.findall(rb"k_files_md5ILi(\d+)ELi(\d+)E", blob)
+    assert em and fm, "kernel names not found in the library"
+    assert all(int(p) == 0 and nib == b"0" and hg == b"0" for _, _, p, nib, hg in em)
+    assert all(int(p) == 0 for _, p in fm)
+    assert "nxec_design_probes" in syms

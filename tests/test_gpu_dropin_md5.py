@@ -172,8 +172,8 @@ print("RESULTS", sorted(map(str, res)), "ALIVE", sum(t.is_alive() for t in th), 
 def test_agent_round_leader_exception_releases_everyone():
     """a leader that throws while building a round must still
     finish the round's jobs with an error and hand leadership on -- no caller
-    may block forever (NXEC_TEST_AGENT_THROW makes every leader throw)."""
-    r = _run(LEADER_THROWS.format(root=ROOT), {"NXEC_TEST_AGENT_THROW": "1"}, timeout=180)
+    may block forever (NXEC_TEST_FAULT=agent_round makes every leader throw)."""
+    r = _run(LEADER_THROWS.format(root=ROOT), {"NXEC_TEST_FAULT": "agent_round"}, timeout=180)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULTS")][0]
     assert "ALIVE 0" in line and line.count(str(_lib.NXEC_ERR_NOMEM)) == 8, line
@@ -251,12 +251,12 @@ def test_decode_object_verify_flags_a_corrupt_chunk(gpu_ctx, where):
 @pytest.mark.gpu
 def test_void_drop_in_retries_after_an_injected_device_error(golden):
     """Option A: rs.cc's ISA-L calls through include/nxec_isal_compat.h with the
-    first attempt of every nxec_ec_encode_data failing (NXEC_TEST_FAIL_ENCODE=1):
+    first attempt of every nxec_ec_encode_data failing (NXEC_TEST_FAULT=encode):
     the retry on a fresh context produces the golden parity, nothing aborts."""
     binary = os.path.join(ROOT, "build", "isal_compat_test")
     c = next(c for c in golden["encode"] if c["n"] == 14 and c["k"] == 10 and c["cs"] == 4096)
     r = subprocess.run([binary, "14", "10", "4096"], capture_output=True, text=True, timeout=120,
-                       env=dict(os.environ, NXEC_TEST_FAIL_ENCODE="1"))
+                       env=dict(os.environ, NXEC_TEST_FAULT="encode"))
     assert r.returncode == 0, r.stderr[-2000:]
     assert "retrying once on a fresh context" in r.stderr
     assert c["parity_sha256"] in r.stdout, r.stdout[-500:]
@@ -302,9 +302,9 @@ print("ONE", h1, g1, "MANY", h2 - h1, g2 - g1, "BAD", len(bad), flush=True)
 def test_auto_placement_moves_many_callers_to_the_gpu():
     """include/nxec.h §2, NXEC_DIGEST_PLACE=auto: a lone caller hashes on the
     host pool; once more threads call than the crossover (here
-    NXEC_DIGEST_HOST_CALLERS=2, so 6 callers > 2H) the calls move to the
+    NXEC_DIGEST_CPUS=2, so 6 callers > 2) the calls move to the
     coding kernel -- every digest and parity byte right either way."""
-    r = _run(AUTO_SWITCH.format(root=ROOT), {"NXEC_DIGEST_HOST_CALLERS": "2", "NXEC_DIGEST_PLACE": "auto"}, timeout=240)
+    r = _run(AUTO_SWITCH.format(root=ROOT), {"NXEC_DIGEST_CPUS": "2", "NXEC_DIGEST_PLACE": "auto"}, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("ONE")][0].split()
     one_h, one_g, many_h, many_g, nbad = int(line[1]), int(line[2]), int(line[4]), int(line[5]), int(line[7])

@@ -4,10 +4,11 @@ The proxy's write path (chunk_manager.cc:66-452) codes each stripe with
 RSCode::encode and then hashes every chunk (Chunk::computeMD5, :175).  The
 fused kernel does both in one pass; bar: parity bit-exact with the oracle
 (the reference's ISA-L arithmetic), digests equal to hashlib's MD5, and both
-byte-identical to the two-kernel path (NXEC_FUSED_MD5=0) on the same inputs.
+byte-identical to the two-kernel path on the same inputs -- the public calls
+the fused kernel replaces (coding through nxec_encode_object / recover without
+digests, then nxec_md5_chunks).
 """
 import hashlib
-import os
 
 import numpy as np
 import pytest
@@ -19,24 +20,43 @@ from nexoedge_amd import nxec
 pytestmark = pytest.mark.gpu
 
 
+def _md5_interleaved(ctx, parts, ns, n):
+    """[ns][n][16] digests from nxec_md5_chunks calls, each part (base,
+    chunk_stride, stripe_stride, nchunks, length, nstripes, first chunk id, first stripe)."""
+    out = np.zeros((ns, n, 16), dtype=np.uint8)
+    for base, cst, sst, nch, length, nst, c0, s0 in parts:
+        if nst == 0 or nch == 0:
+            continue
+        d = nxec.DeviceBuffer(nst * nch * 16)
+        ctx.md5_chunks(base, cst, sst, nch, length, nst, d.ptr)
+        ctx.sync()
+        out[s0:s0 + nst, c0:c0 + nch] = d.download().reshape(nst, nch, 16)
+        d.free()
+    return out
+
+
 def _encode_object(ctx, n, k, M, obj_buf, length, fused):
+    """nxec_encode_object with digests (fused: the full stripes through
+    k_mul_md5), or -- the two-kernel reference -- the same call without digests
+    followed by nxec_md5_chunks over the object, the tail arena and the parity."""
     ns, nf, cl = nxec.object_layout(n, k, length, M)
     p = n - k
     par = nxec.DeviceBuffer(max(ns * p * M, 1))
     tail = nxec.DeviceBuffer(k * M)
     md5 = nxec.DeviceBuffer(ns * n * 16 + 3)
-    old = os.environ.get("NXEC_FUSED_MD5")
-    os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
-    try:
+    if fused:
         # digests at an odd address: the kernel writes them byte-wise
         ctx.encode_object(n, k, obj_buf.ptr, length, M, par.ptr, tail.ptr, md5.ptr + 3)
         ctx.sync()
-    finally:
-        if old is None:
-            del os.environ["NXEC_FUSED_MD5"]
-        else:
-            os.environ["NXEC_FUSED_MD5"] = old
-    out = par.download().reshape(ns, p, M), md5.download()[3:].reshape(ns, n, 16)
+        dig = md5.download()[3:].reshape(ns, n, 16)
+    else:
+        ctx.encode_object(n, k, obj_buf.ptr, length, M, par.ptr, tail.ptr, None)
+        ctx.sync()
+        t = ns - nf
+        dig = _md5_interleaved(ctx, [(obj_buf.ptr, M, k * M, k, M, nf, 0, 0), (par.ptr, M, p * M, p, M, nf, k, 0),
+                                     (tail.ptr, cl, k * cl, k, cl, t, 0, nf),
+                                     (par.ptr + nf * p * M, M, p * M, p, cl, t, k, nf)], ns, n)
+    out = par.download().reshape(ns, p, M), dig
     for b in (par, tail, md5):
         b.free()
     return out
@@ -110,17 +130,21 @@ def test_fused_encode_md5_full_batch(gpu_ctx):
     dig = [nxec.DeviceBuffer(ns * n * 16) for _ in range(2)]
     sums = []
     for fused in (True, False):
-        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
-        try:
-            par.memset(0)
-            gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, None, dig[0 if fused else 1].ptr)
-            gpu_ctx.sync()
-        finally:
-            del os.environ["NXEC_FUSED_MD5"]
+        par.memset(0)
+        if fused:
+            gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, None, dig[0].ptr)
+        else:  # the two kernels: coding, then the MD5 of the object's and the parity's chunks
+            gpu_ctx.encode_object(n, k, ob.ptr, length, M, par.ptr, None, None)
+            gpu_ctx.md5_chunks(ob.ptr, M, k * M, k, M, ns, dig[1].ptr)
+        gpu_ctx.sync()
         sums.append(par.checksum())
     assert sums[0] == sums[1]
     d0 = dig[0].download().reshape(ns, n, 16)
-    d1 = dig[1].download().reshape(ns, n, 16)
+    dpar = nxec.DeviceBuffer(ns * p * 16)
+    gpu_ctx.md5_chunks(par.ptr, M, p * M, p, M, ns, dpar.ptr)
+    gpu_ctx.sync()
+    d1 = np.concatenate([dig[1].download(ns * k * 16).reshape(ns, k, 16), dpar.download().reshape(ns, p, 16)], axis=1)
+    dpar.free()
     assert np.array_equal(d0, d1)
     for s in (0, 1777, ns - 1):
         data = ob.download(k * M, offset=s * k * M)
@@ -182,7 +206,7 @@ def test_rs_encode_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns):
 def test_rs_recover_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns, failed):
     """Repair with checksums (rs.cc:238-322 + Chunk::computeMD5, chunk_manager.cc:1173):
     the rebuilt chunks equal the oracle's encode of the same data, their digests
-    equal hashlib's, and fused == recover + MD5 launches (NXEC_FUSED_MD5=0)."""
+    equal hashlib's, and fused == recover + nxec_md5_chunks of the rebuilt chunks."""
     data = fill_bytes(ns * k * cs, 313 + cs + len(failed)).reshape(ns, k, cs)
     full = np.zeros((ns, sstride), dtype=np.uint8)
     for s in range(ns):
@@ -198,13 +222,16 @@ def test_rs_recover_md5_stripes(gpu_ctx, n, k, cs, cstride, sstride, ns, failed)
         b = nxec.DeviceBuffer(damaged.nbytes)
         b.upload(damaged)
         d = nxec.DeviceBuffer(ns * len(failed) * 16)
-        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
-        try:
+        if fused:
             gpu_ctx.rs_recover_md5(n, k, failed, b.ptr, cstride, sstride, cs, ns, d.ptr)
             gpu_ctx.sync()
-        finally:
-            del os.environ["NXEC_FUSED_MD5"]
-        outs.append((b.download().reshape(ns, sstride), d.download().reshape(ns, len(failed), 16)))
+            dig = d.download().reshape(ns, len(failed), 16)
+        else:
+            gpu_ctx.rs_recover(n, k, failed, b.ptr, cstride, sstride, cs, ns)
+            gpu_ctx.sync()
+            dig = _md5_interleaved(gpu_ctx, [(b.ptr + f * cstride, cstride, sstride, 1, cs, ns, r, 0)
+                                             for r, f in enumerate(failed)], ns, len(failed))
+        outs.append((b.download().reshape(ns, sstride), dig))
         b.free()
         d.free()
     assert np.array_equal(outs[0][0], full)
@@ -236,12 +263,12 @@ def test_rs_recover_md5_full_batch(gpu_ctx):
         gpu_ctx.sync()
         assert buf.checksum() != ref
         d = nxec.DeviceBuffer(ns * 16)
-        os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
-        try:
+        if fused:
             gpu_ctx.rs_recover_md5(n, k, [0], buf.ptr, cst, sst, cs, ns, d.ptr)
-            gpu_ctx.sync()
-        finally:
-            del os.environ["NXEC_FUSED_MD5"]
+        else:
+            gpu_ctx.rs_recover(n, k, [0], buf.ptr, cst, sst, cs, ns)
+            gpu_ctx.md5_chunks(buf.ptr, cst, sst, 1, cs, ns, d.ptr)
+        gpu_ctx.sync()
         assert buf.checksum() == ref
         digs.append(d.download().reshape(ns, 16))
         d.free()
@@ -269,11 +296,12 @@ def _object_chunks(n, k, M, obj, par_h, length):
 
 
 @pytest.mark.parametrize("failed", [[], [1, 4, 11, 13], [10, 11], [0, 1, 2, 3]])
-@pytest.mark.parametrize("fused", [True, False])
-def test_decode_object_verify(gpu_ctx, failed, fused):
+def test_decode_object_verify(gpu_ctx, failed):
     """Read path with checksums (Chunk::verifyMD5 of every fetched chunk,
-    chunk_manager.cc:1548-1556, then decodeFile): the object comes back intact,
-    every chunk read is flagged ok, a corrupted input is flagged and counted."""
+    chunk_manager.cc:1548-1556, then decodeFile), fused verify + decode: the
+    object comes back intact, every chunk read is flagged ok, a corrupted
+    input is flagged and counted.  (The verify launches + decode form runs in
+    test_decode_object_verify_many_losses.)"""
     n, k, M = 14, 10, 65536
     length = 5 * k * M + 77777
     obj = fill_bytes(length, 6060 + len(failed))
@@ -298,12 +326,8 @@ def test_decode_object_verify(gpu_ctx, failed, fused):
     ok.memset(7)
     nb = nxec.DeviceBuffer(8)
     nb.memset(0)
-    os.environ["NXEC_FUSED_MD5"] = "1" if fused else "0"
-    try:
-        gpu_ctx.decode_object_verify(n, k, failed, cb.ptr, length, M, md5.ptr, out.ptr, tail.ptr, ok.ptr, nb.ptr)
-        gpu_ctx.sync()
-    finally:
-        del os.environ["NXEC_FUSED_MD5"]
+    gpu_ctx.decode_object_verify(n, k, failed, cb.ptr, length, M, md5.ptr, out.ptr, tail.ptr, ok.ptr, nb.ptr)
+    gpu_ctx.sync()
     flags = ok.download().reshape(ns, n)
     want = np.full((ns, n), 7, dtype=np.uint8)
     want[:, alive] = 1

@@ -172,7 +172,11 @@ def test_stripes_mul_vs_oracle(gpu_ctx, rows, k, length, nstripes):
 
 @pytest.mark.parametrize("lds_r", ["1", "8", "16"])
 def test_lds_replication_variants_agree(gpu_ctx, monkeypatch, lds_r):
-    """All LDS-replication variants (tuning knob) are bit-identical."""
+    """All LDS-replication variants (a design-probe knob, `make PROBES=1`) are
+    bit-identical; the product build chooses R by k, which the k = 1..127
+    sweeps cover."""
+    if not nxec.design_probes():
+        pytest.skip("library built without the design-probe knobs (make PROBES=1)")
     monkeypatch.setenv("NXEC_LDS_R", lds_r)
     rows, k, length, ns = 4, 10, 1 << 14, 3
     rng = np.random.default_rng(11)
@@ -682,16 +686,17 @@ def test_survey_named_encode_entry_points(gpu_ctx):
     pb.free()
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("misalign,n,k,M", [(0, 9, 6, 4096), (3, 9, 6, 4096), (0, 9, 6, 1000), (0, 14, 10, 65536),
-                                             (5, 14, 10, 16400), (0, 24, 20, 4096), (0, 6, 6, 4096)])
-def test_encode_objects_matches_per_object(gpu_ctx, monkeypatch, fused, misalign, n, k, M):
-    """Many objects per call (full stripes in one gather launch, last stripes in
-    one ragged work-queue launch -- the list kernel for k > 19 --, MD5 of every
-    chunk in one list launch) equals encoding each object on its own with
+                                             (5, 14, 10, 16400), (0, 24, 20, 4096), (0, 6, 6, 4096),
+                                             (0, 15, 10, 4096), (0, 16, 10, 2048)])
+def test_encode_objects_matches_per_object(gpu_ctx, misalign, n, k, M):
+    """Many objects per call equals encoding each object on its own with
     nxec_encode_object; the tail arena holds the zero-padded last-stripe chunks.
-    fused = "1": aligned batches with k <= 16 run as one k_files_md5 launch."""
-    monkeypatch.setenv("NXEC_FUSED_MD5", fused)
+    Aligned batches with k <= 16 and p <= 4 run as one k_files_md5 launch;
+    misaligned objects, chunk sizes not a multiple of 16, k > 16 and p > 4
+    take the separate launches (full stripes in one gather or list launch,
+    last stripes through the pad copy and one ragged work-queue launch -- the
+    list kernel for k > 19 --, the MD5 of every chunk in one list launch)."""
     p = n - k
     lengths = [0, 1, 17, k * M - 1, k * M, 3 * k * M + 100, 5000, 2 * k * M, 12345]
     total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
@@ -1222,13 +1227,36 @@ def test_config1_both_readings_golden(gpu_ctx, golden, n, k, cs):
     par.free()
 
 
+def _encode_objects_out(ctx, n, k, M, ptrs, lengths, separate, tail_fill=0, flags=0):
+    """nxec_encode_objects_ex -> (parity [total][p][M], tail arena, digests
+    [total][n][16]).  separate: the parity slots at an odd address, which
+    takes the library's separate launches (pad copy, list coding, MD5 list)
+    instead of the one k_files_md5 launch, on the same objects."""
+    p = n - k
+    total, tail_bytes = nxec.objects_layout(n, k, lengths, M)
+    off = 1 if separate else 0
+    par = nxec.DeviceBuffer(total * p * M + off)
+    par.memset(0)
+    tail = nxec.DeviceBuffer(max(tail_bytes, 16))
+    tail.memset(tail_fill)
+    md5 = nxec.DeviceBuffer(total * n * 16)
+    ctx.encode_objects(n, k, ptrs, lengths, M, par.ptr + off, tail.ptr, md5.ptr, flags=flags)
+    ctx.sync()
+    out = (par.download()[off:].reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
+    for b in (par, tail, md5):
+        b.free()
+    return out
+
+
 @pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (20, 16, 8192), (6, 4, 4096), (5, 1, 1024), (9, 6, 4112),
                                    (7, 3, 208)])
-def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, k, M):
+def test_encode_objects_fused_equals_separate_launches(gpu_ctx, n, k, M):
     """Hundreds of files of random sizes (1 B .. 3 full stripes): the one-launch
     multi-file write (k_files_md5, requests sorted longest first, per-request
     lengths) gives the same parity, tail arena and digests as the separate
-    gather / pad / ragged / MD5-list launches, and the digests match hashlib."""
+    gather / pad / list / MD5-list launches -- which the library takes for the
+    same objects when the parity slots are not 16-byte aligned (_separate) --
+    and the digests match hashlib."""
     import hashlib
     p = n - k
     rng = np.random.default_rng(n * 1000 + M)
@@ -1240,17 +1268,8 @@ def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, 
         pos += (L + 15) // 16 * 16
     host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
     arena = up(host)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("NXEC_FUSED_MD5", mode)
-        par = nxec.DeviceBuffer(total * p * M)
-        par.memset(0)
-        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
-        md5 = nxec.DeviceBuffer(total * n * 16)
-        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
-        out[mode] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
-        for b in (par, tail, md5):
-            b.free()
+    out = {mode: _encode_objects_out(gpu_ctx, n, k, M, [arena.ptr + o for o in offs], lengths, mode == "0")
+           for mode in ("1", "0")}
     (p1, t1, m1), (p0, t0, m0) = out["1"], out["0"]
     assert np.array_equal(t1, t0)
     assert np.array_equal(m1, m0)
@@ -1273,13 +1292,13 @@ def test_encode_objects_fused_equals_separate_launches(gpu_ctx, monkeypatch, n, 
 
 
 @pytest.mark.parametrize("n,k,M", [(14, 10, 65536), (6, 4, 4096), (20, 16, 2048), (5, 1, 1024)])
-def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, M):
-    """The one-launch write reads every last stripe straight from its object
-    (no pad copy): objects shorter than a stripe at every byte offset, chunk
-    lengths around the kernel's 256-byte steps (the last step's 16th lane
-    fetches the line after its own) and partial / empty data chunks.  Parity,
-    the zero-padded tail arena and every digest equal the separate launches
-    (pad copy + ragged + MD5 list) and the oracle / hashlib."""
+def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, n, k, M):
+    """The one-launch write reads every last stripe in place from its object:
+    objects shorter than a stripe at every byte offset, chunk lengths around
+    the kernel's 256-byte steps (the last step's 16th lane fetches the line
+    after its own) and partial / empty data chunks.  Parity, the zero-padded
+    tail arena and every digest equal the separate launches (pad copy + list
+    coding + MD5 list) and the oracle / hashlib."""
     import hashlib
     p = n - k
     rng = np.random.default_rng(7 * n + M)
@@ -1300,25 +1319,11 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
     arena = up(host)
     total, tail_bytes = nxec.objects_layout(n, k, lens, M)
     assert total == len(lens)
-    out = {}
-    for mode in ("1", "pad", "0"):  # tails read in the kernel / pad copy first (NXEC_FILES_TAIL=0) / separate launches
-        monkeypatch.setenv("NXEC_FUSED_MD5", "0" if mode == "0" else "1")
-        monkeypatch.setenv("NXEC_FILES_TAIL", "0" if mode == "pad" else "1")
-        par = nxec.DeviceBuffer(total * p * M)
-        par.memset(0)
-        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
-        tail.memset(0xAB)
-        md5 = nxec.DeviceBuffer(total * n * 16)
-        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lens, M, par.ptr, tail.ptr, md5.ptr)
-        gpu_ctx.sync()
-        out[mode] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
-        for b in (par, tail, md5):
-            b.free()
+    out = {mode: _encode_objects_out(gpu_ctx, n, k, M, [arena.ptr + o for o in offs], lens, mode == "0", tail_fill=0xAB)
+           for mode in ("1", "0")}
     (p1, t1, m1), (p0, t0, m0) = out["1"], out["0"]
-    for other in ("pad", "0"):
-        po, to, mo = out[other]
-        assert np.array_equal(t1[:tail_bytes], to[:tail_bytes]), other
-        assert np.array_equal(m1, mo), other
+    assert np.array_equal(t1[:tail_bytes], t0[:tail_bytes])
+    assert np.array_equal(m1, m0)
     toff = 0
     for i, (o, L) in enumerate(zip(offs, lens)):
         ns, nf, cl = nxec.object_layout(n, k, L, M)
@@ -1330,7 +1335,6 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
         got = t1[toff:toff + k * cls].reshape(k, cls)
         assert np.array_equal(got[:, :cl], chunks) and not got[:, cl:].any(), (i, L)
         assert np.array_equal(p1[i, :, :cl], p0[i, :, :cl]), (i, L)
-        assert np.array_equal(p1[i, :, :cl], out["pad"][0][i, :, :cl]), (i, L)
         if i % 7 == 0:
             par_want = oracle.rs_encode(n, k, want, cl)
             for r in range(p):
@@ -1343,13 +1347,12 @@ def test_encode_objects_tail_from_unaligned_objects(gpu_ctx, monkeypatch, n, k, 
 
 
 @pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 6000), (16, 12, 2048, 9000), (6, 4, 1024, 5000)])
-def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
+def test_encode_objects_slot_packing(gpu_ctx, n, k, M, nfiles):
     """More requests than the chip has slots (256 CUs x 16): the planner packs
     several requests into a slot (longest first into the least loaded one) and
     each lane's cursor walks them back to back.  Parity, tail arena and every
-    digest equal the separate launches (NXEC_FUSED_MD5=0) and the
-    one-request-per-slot form (NXEC_FILES_PACK=0, a second workgroup wave);
-    every digest of a sample of stripes equals hashlib's."""
+    digest equal the separate launches (unaligned parity slots); every digest
+    of a sample of stripes equals hashlib's."""
     import hashlib
     p = n - k
     rng = np.random.default_rng(nfiles + n)
@@ -1361,20 +1364,10 @@ def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
         pos += (L + 15) // 16 * 16
     host = rng.integers(0, 256, size=pos + 16, dtype=np.uint8)
     arena = up(host)
-    out = {}
-    for fused, pack in (("1", "1"), ("1", "0"), ("0", "1")):
-        monkeypatch.setenv("NXEC_FUSED_MD5", fused)
-        monkeypatch.setenv("NXEC_FILES_PACK", pack)
-        par = nxec.DeviceBuffer(total * p * M)
-        par.memset(0)
-        tail = nxec.DeviceBuffer(max(tail_bytes, 16))
-        md5 = nxec.DeviceBuffer(total * n * 16)
-        gpu_ctx.encode_objects(n, k, [arena.ptr + o for o in offs], lengths, M, par.ptr, tail.ptr, md5.ptr)
-        out[fused + pack] = (par.download().reshape(total, p, M), tail.download(), md5.download().reshape(total, n, 16))
-        for b in (par, tail, md5):
-            b.free()
+    out = {key: _encode_objects_out(gpu_ctx, n, k, M, [arena.ptr + o for o in offs], lengths, key == "01")
+           for key in ("11", "01")}
     p1, t1, m1 = out["11"]
-    for key in ("10", "01"):
+    for key in ("01",):
         pk, tk, mk = out[key]
         assert np.array_equal(t1, tk), key
         assert np.array_equal(m1, mk), key
@@ -1384,8 +1377,7 @@ def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
         ns, nf, cl = nxec.object_layout(n, k, L, M)
         for s in range(ns):
             cs = M if s < nf else cl
-            for key in ("10", "01"):
-                assert np.array_equal(p1[g + s, :, :cs], out[key][0][g + s, :, :cs]), (key, i, s)
+            assert np.array_equal(p1[g + s, :, :cs], out["01"][0][g + s, :, :cs]), (i, s)
             if i % 97 == 0:  # hashlib on a sample: data chunks from the object / tail arena, parity
                 cls = (cl + 15) // 16 * 16
                 for c in range(k):
@@ -1401,16 +1393,16 @@ def test_encode_objects_slot_packing(gpu_ctx, monkeypatch, n, k, M, nfiles):
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
-def test_encode_objects_async_pipeline(gpu_ctx, monkeypatch, fused):
+def test_encode_objects_async_pipeline(gpu_ctx, fused):
     """NXEC_OBJECTS_ASYNC (include/nxec.h): six different batches queued back to
     back on the context stream -- more than the context's four staging slots,
     so later calls wait for earlier ones' slots -- equal the synchronous calls'
     parity, tails and digests; the host length arrays are rebuilt between calls
     (the call consumed them).  nxec_kernel_time counts one timed launch per call
-    with a positive device time.  fused = 0: the separate launches
-    (NXEC_FUSED_MD5=0) take the same asynchronous exit."""
-    monkeypatch.setenv("NXEC_FUSED_MD5", fused)
+    with a positive device time.  fused = 0: the separate launches (parity
+    slots at an odd address) take the same asynchronous exit."""
     n, k, M = 14, 10, 16384
+    poff = 0 if fused == "1" else 1
     p = n - k
     batches = []
     for b in range(6):
@@ -1426,16 +1418,16 @@ def test_encode_objects_async_pipeline(gpu_ctx, monkeypatch, fused):
         if timing:
             gpu_ctx.kernel_timing(True)
         for lengths, ptrs, total, tail_bytes, _ in batches:
-            par, tail, md5 = (nxec.DeviceBuffer(total * p * M), nxec.DeviceBuffer(max(tail_bytes, 16)),
+            par, tail, md5 = (nxec.DeviceBuffer(total * p * M + poff), nxec.DeviceBuffer(max(tail_bytes, 16)),
                               nxec.DeviceBuffer(total * n * 16))
             tail.memset(0)
-            gpu_ctx.encode_objects(n, k, ptrs, list(lengths), M, par.ptr, tail.ptr, md5.ptr, flags=flags)
+            gpu_ctx.encode_objects(n, k, ptrs, list(lengths), M, par.ptr + poff, tail.ptr, md5.ptr, flags=flags)
             bufs.append((par, tail, md5))
         gpu_ctx.sync()
         kt = gpu_ctx.kernel_time() if timing else None
         if timing:
             gpu_ctx.kernel_timing(False)
-        out = [tuple(b.download() for b in t) for t in bufs]
+        out = [(t[0].download()[poff:],) + tuple(b.download() for b in t[1:]) for t in bufs]
         for t in bufs:
             for b in t:
                 b.free()
@@ -1591,4 +1583,69 @@ def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
                     assert m1[g + ns - 1, j].tobytes() == hashlib.md5(data.tobytes()).digest(), (i, j)
             toff += k * cls
         g += ns
+    arena.free()
+
+
+@pytest.mark.parametrize("flags", [0, "inplace"])
+def test_encode_objects_last_stripe_at_a_page_end(gpu_ctx, flags):
+    """Last stripes read in place (k_files_md5's masked chunk) never touch a
+    4 KiB page the object does not: objects that end 1..15 bytes before a page
+    boundary, with chunk lengths that are not a multiple of 16 (a whole chunk's
+    last vector runs up to 15 bytes past it) and partial chunks of 1..15 bytes
+    -- the case that falls back to the pad copy for the chunks from the
+    overrunning one on -- mixed with ordinary ones.  Parity, the tail arena
+    (all of it without the flag, the partial chunk with it) and every digest
+    equal the separate launches, the oracle and hashlib."""
+    import hashlib
+    fl = nxec.OBJECTS_TAIL_INPLACE if flags == "inplace" else 0
+    n, k, M = 14, 10, 4096
+    p = n - k
+    picks = []  # (length, gap to the page end)
+    for L in range(200, 9 * M):
+        cl = -(-L // k)
+        cls = (cl + 15) // 16 * 16
+        jf, last = L // cl, L % cl
+        for gap in (1, 7, 15):
+            if 0 < jf < k and cls - cl > last + gap:
+                picks.append((L, gap))
+        if len(picks) >= 24:
+            break
+    picks += [(L, 3) for L in (1000, 4095, 9999, 12345)]
+    assert len(picks) >= 24
+    page = 4096
+    npages = [(L + 16) // page + 1 for L, _ in picks]
+    arena = nxec.DeviceBuffer(page * (sum(npages) + 2))
+    offs = []
+    base = (-arena.ptr) % page  # first page boundary inside the buffer
+    end_page = 0
+    for (L, gap), np_ in zip(picks, npages):  # each object ends `gap` bytes before a page boundary
+        end_page += np_
+        offs.append(base + end_page * page - gap - L)
+    assert all(o >= 0 for o in offs) and all(offs[i] + picks[i][0] <= offs[i + 1] for i in range(len(picks) - 1))
+    host = np.random.default_rng(5).integers(0, 256, size=arena.nbytes, dtype=np.uint8)
+    arena.upload(host)
+    lengths = [L for L, _ in picks]
+    ptrs = [arena.ptr + o for o in offs]
+    p1, t1, m1 = _encode_objects_out(gpu_ctx, n, k, M, ptrs, lengths, False, tail_fill=0xAB, flags=fl)
+    p0, t0, m0 = _encode_objects_out(gpu_ctx, n, k, M, ptrs, lengths, True, tail_fill=0xAB)
+    assert np.array_equal(m1, m0)
+    toff = 0
+    for i, (o, L) in enumerate(zip(offs, lengths)):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        assert (ns, nf) == (1, 0)
+        cls = (cl + 15) // 16 * 16
+        want = np.zeros(k * cl, dtype=np.uint8)
+        want[:L] = host[o:o + L]
+        chunks = want.reshape(k, cl)
+        assert np.array_equal(p1[i, :, :cl], p0[i, :, :cl]), (i, L)
+        par_want = oracle.rs_encode(n, k, want, cl)
+        for r in range(p):
+            assert np.array_equal(p1[i, r, :cl], par_want[k + r]), (i, L, r)
+        slots = t1[toff:toff + k * cls].reshape(k, cls)
+        jf, part = L // cl, L % cl
+        for j in range(k):
+            if fl == 0 or (j == jf and part) or (slots[j] != 0xAB).any():
+                assert np.array_equal(slots[j, :cl], chunks[j]) and not slots[j, cl:].any(), (i, L, j)
+            assert m1[i, j].tobytes() == hashlib.md5(chunks[j].tobytes()).digest(), (i, L, j)
+        toff += k * cls
     arena.free()

@@ -43,7 +43,8 @@ def rate(n, k, cs, cstride, sstride, op):
 
 
 geoms = [tuple(int(x) for x in g.split(",")) for g in sys.argv[1:]] or [(14, 10, 1024), (20, 16, 4096)]
-for n, k, cs_kib in geoms:
+# PROBE_REPEAT=R walks the whole sweep R times (alternating A/B on one box)
+for n, k, cs_kib in geoms * int(os.environ.get("PROBE_REPEAT", "1")):
     cs = cs_kib << 10
     p = n - k
     pats = ["encode", list(range(p)), list(range(k, n)), [1, 4, n - 3, n - 1][:p]]
@@ -55,8 +56,12 @@ for n, k, cs_kib in geoms:
     for cpad in cpads:
         cstride = cs + cpad
         for spad_chunks in spads:
-            sstride = n * cstride + int(spad_chunks * cstride) // 4096 * 4096
-            for sg in (sgs if cs >= (2 << 20) else ["1"]):
+            # whole chunks of stripe padding exactly (an odd stripe stride in
+            # units of the chunk stride); fractions rounded down to 4 KiB
+            extra = int(spad_chunks) * cstride if spad_chunks == int(spad_chunks) else \
+                int(spad_chunks * cstride) // 4096 * 4096
+            sstride = n * cstride + extra
+            for sg in (sgs if cs >= (2 << 20) or os.environ.get("PROBE_SG_ALL") else ["1"]):
                 os.environ["NXEC_STRIPE_GROUP"] = sg
                 res = [rate(n, k, cs, cstride, sstride, op) for op in pats]
                 fr = [f for _, f in res]
