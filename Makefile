@@ -8,7 +8,7 @@ CXXSTD   := -std=c++17
 # PROBES=1 adds the design-probe kernels (DESIGN.md section 4 A/Bs; `make clean` first)
 PROBES   ?= 0
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC $(CXXSTD) -Wall -Iinclude -Inexoedge_amd/csrc \
-            -mllvm -amdgpu-atomic-optimizer-strategy=None -DNXEC_DESIGN_PROBES=$(PROBES)
+            -mllvm -amdgpu-atomic-optimizer-strategy=None -DNXEC_DESIGN_PROBES=$(PROBES) $(EXTRA_FLAGS)
 LIBDIR   := nexoedge_amd/lib
 CSRC     := nexoedge_amd/csrc
 OBJDIR   := build/obj

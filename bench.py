@@ -60,10 +60,13 @@ def parse(argv=None):
                          "repair12 = config 4; mixed16 = config 5 (one chunk size)")
     ap.add_argument("--failed", type=int, default=None, help="repair12: failed chunk id (default 0)")
     ap.add_argument("--gib", type=float, default=32.0, help="mixed16: GiB of stripes per GPU")
-    ap.add_argument("--layout", choices=["auto", "natural", "recover"], default="auto",
+    ap.add_argument("--group", action="store_true",
+                    help="rs10_4 only: also drive all N GPUs from ONE process through nxec_group (one host thread "
+                         "+ context per device); reported as `group` beside the per-rank value, not as value")
+    ap.add_argument("--layout", choices=["auto", "natural", "recover", "tuned"], default="auto",
                     help="HBM batch layout: natural = packed [stripe][n][cs]; auto = nxec_batch_layout (padded "
                          "chunk stride for chunks >= 2 MiB); recover = nxec_batch_layout(RECOVER_HEAVY) (odd "
-                         "stripe stride in 1 MiB units)")
+                         "stripe stride in 1 MiB units); tuned = nxec_batch_layout_tuned (measured on this device)")
     return ap.parse_args(argv)
 
 
@@ -299,10 +302,13 @@ def _zero_chunks(buf, chunks, cst, stripe, cs, ns, stream):
         buf.memset2d(0, c * cst, stripe, cs, ns, stream)
 
 
-def layout(args, n, cs):
+def layout(args, n, cs, ctx=None, k=None):
     """(chunk_stride, stripe_stride, description) of the batch layout --layout selects."""
     if args.layout == "natural":
         return cs, n * cs, "packed [stripe][n][cs]"
+    if args.layout == "tuned":
+        c, st = ctx.batch_layout_tuned(n, k, cs)
+        return c, st, f"nxec_batch_layout_tuned: chunk stride {c} B, stripe stride {st} B (measured on this device)"
     flags = nxec.LAYOUT_RECOVER_HEAVY if args.layout == "recover" else 0
     c, st = nxec.batch_layout(n, cs, flags)
     return c, st, f"nxec_batch_layout({args.layout}): chunk stride {c} B, stripe stride {st} B"
@@ -312,7 +318,7 @@ def wl_rs10_4(args, ctx, stream, rank):
     """Configs 2+3: RS(10,4) encode + 4-erasure recover, 1 MiB chunks, 4096 stripes."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
     p, e = n - k, len(PATTERNS[0])
-    cst, stripe, lay = layout(args, n, cs)
+    cst, stripe, lay = layout(args, n, cs, ctx, k)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xC0FFEE + rank * 7919)  # synthetic data; parity region overwritten by encode
     ops = [
@@ -348,7 +354,7 @@ def wl_decode_full(args, ctx, stream, rank):
     the surviving ones passed through (unit rows of the inverse).  4 erasures,
     rotating over the headline's three patterns; 2k*cs per stripe."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
-    cst, stripe, lay = layout(args, n, cs)
+    cst, stripe, lay = layout(args, n, cs, ctx, k)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xDEC0DE + rank * 7919)
     ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream)
@@ -384,7 +390,7 @@ def wl_repair12(args, ctx, stream, rank):
     unfused agent partial-encode path (racks of 4 chunks: partial 1 x g encodes,
     container_manager.cc:251, then the CAR XOR finalize, rs.cc:94-109)."""
     n, k, cs, ns, g = 16, 12, args.chunk, args.stripes, 4
-    cst, stripe, lay = layout(args, n, cs)
+    cst, stripe, lay = layout(args, n, cs, ctx, k)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xBEEF + rank)
     ctx.rs_encode(n, k, buf.ptr, cst, stripe, cs, ns, stream)
@@ -417,7 +423,7 @@ def wl_mixed16(args, ctx, stream, rank):
     """Config 5: RS(16,4) alternating encode / 4-erasure decode at one chunk size;
     the stripe count fills ~args.gib GiB per GPU."""
     n, k, cs = 20, 16, args.chunk
-    cst, stripe, lay = layout(args, n, cs)
+    cst, stripe, lay = layout(args, n, cs, ctx, k)
     ns = max(1, int(args.gib * (1 << 30)) // stripe)
     buf = nxec.DeviceBuffer(ns * stripe)
     buf.fill_random(0xFACE + rank)
@@ -732,6 +738,77 @@ def launch_local_ranks(argv, world):
     return 0
 
 
+def group_devices(members, visible):
+    """Device of each nxec_group member: member i on GPU i, round-robin when
+    fewer GPUs are visible (the one-GPU box rehearses an 8-member group)."""
+    return [i % max(1, visible) for i in range(members)]
+
+
+def group_measure(args):
+    """--group: the one-process deployment of SURVEY §8e ("one host thread +
+    hipSetDevice + streams per GPU"): an nxec_group of N contexts, member i
+    owning its own args.stripes-stripe batch on device i (weak scaling, as the
+    ranks), each step the headline's encode + recover (rotating patterns)
+    through nxec_group_rs_{encode,recover}_stripes -- one host thread per
+    member per call, every call synchronous.  Verified as the ranks' run: the
+    batches' checksums survive the timed steps, and erased chunks of every
+    member come back.  Aggregate user-visible GiB/s of all members."""
+    n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
+    p, e = n - k, len(PATTERNS[0])
+    devices = group_devices(args.gpus, nxec.device_count())
+    # the table's layout for "tuned" too (the calibration runs on one context)
+    cst, stripe, lay = layout(argparse.Namespace(**dict(vars(args), layout="auto" if args.layout == "tuned"
+                                                        else args.layout)), n, cs)
+    g = nxec.Group(devices)
+    bufs = []
+    for i, d in enumerate(devices):
+        nxec.set_device(d)
+        b = nxec.DeviceBuffer(ns * stripe)
+        b.fill_random(0x6A0 + 7919 * i)
+        bufs.append(b)
+    ptrs, counts = [b.ptr for b in bufs], [ns] * len(devices)
+    g.rs_encode(n, k, ptrs, cst, stripe, cs, counts)
+
+    def sums():
+        out = []
+        for d, b in zip(devices, bufs):
+            nxec.set_device(d)
+            out.append(b.checksum())
+        return out
+
+    def step(i):
+        g.rs_encode(n, k, ptrs, cst, stripe, cs, counts)
+        g.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], ptrs, cst, stripe, cs, counts)
+
+    for i in range(max(1, args.warmup)):
+        step(i)
+    want = sums()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    dt = time.perf_counter() - t0
+    verified = sums() == want
+    # erase the third pattern's chunks in every member's batch for real, rebuild them
+    for d, b in zip(devices, bufs):
+        nxec.set_device(d)
+        for c in PATTERNS[2]:
+            b.memset2d(0, c * cst, stripe, cs, ns)
+    nxec.device_sync()
+    destroyed = all(a != w for a, w in zip(sums(), want))
+    g.rs_recover(n, k, PATTERNS[2], ptrs, cst, stripe, cs, counts)
+    verified = verified and destroyed and sums() == want
+    step_bytes = len(devices) * ns * ((k + p) + (k + e)) * cs
+    for d, b in zip(devices, bufs):
+        nxec.set_device(d)
+        b.free()
+    g.close()
+    return {"value": round(step_bytes * args.steps / dt / GIB, 2), "unit": "GiB/s", "members": len(devices),
+            "devices": devices, "stripes_per_member": ns, "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "verified": verified, "layout": lay,
+            "note": "one process, nxec_group: a host thread + context per member, each call synchronous; "
+                    "encode (k+p)*cs + recover (k+e)*cs per stripe as the headline"}
+
+
 def dry_run(args):
     """Launcher/rendezvous check without a GPU: the ranks meet over gloo, take
     the same barrier + max-over-ranks + sum reductions as a real run, and rank
@@ -746,8 +823,12 @@ def dry_run(args):
     elapsed = grp.max(t)
     ranks = grp.sum(1.0)
     if grp.rank == 0:
-        print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": grp.world, "ranks_seen": int(ranks),
-                          "max_elapsed_s": elapsed, "steps": args.steps, "warmup": args.warmup}), flush=True)
+        line = {"metric": "dry-run", "value": None, "n_gpus": grp.world, "ranks_seen": int(ranks),
+                "max_elapsed_s": elapsed, "steps": args.steps, "warmup": args.warmup}
+        if args.group:  # the one-process deployment's plan: member i on device i, its own stripe batch
+            line["group"] = {"members": args.gpus, "devices": group_devices(args.gpus, args.gpus),
+                             "stripes_per_member": args.stripes}
+        print(json.dumps(line), flush=True)
     grp.close()
 
 
@@ -918,10 +999,16 @@ def main():
             "kind": "reference" if ref_v is not None else "port",
             "sample": f"one 4 MiB file written and read back, {CONFIG1[0][3]}; both readings in by_config",
             "by_config": by, "host": _host_info()}
-    if rank == 0:
-        print(json.dumps(result), flush=True)
     for b in wl.buffers:
         b.free()
+    if args.group and wl.name == "rs10_4":
+        # the one-process deployment over the same GPUs, after the ranks' buffers are gone
+        grp.barrier()
+        if rank == 0:
+            result["group"] = group_measure(args)
+        grp.barrier()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
     ctx.close()
     grp.close()
 
@@ -968,7 +1055,9 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     hd.free()
     hp.free()
     hm.free()
-    out["read_frames_decode_GiB_s_user_data"] = round(read_from_frames(ctx, n, k, cs, min(ns, 128)), 2)
+    rf = read_from_frames(ctx, n, k, cs, min(ns, 256))
+    out["read_frames_decode_GiB_s_user_data"] = rf["pipelined"]
+    out["read_frames_decode_legs"] = rf
     out["recover_frames_zero_copy"] = recover_frames_rate(ctx, n, k, cs, min(ns, 128))
     return out
 
@@ -1012,54 +1101,60 @@ def host_inclusive_ranks(ctx, grp, n, k, cs, ns=256, reps=3):
             "note": "zero copy over each GPU's own PCIe link, all ranks at once (slowest rank's time)"}
 
 
-def read_from_frames(ctx, n, k, cs, ns, readers=1):
+def read_from_frames(ctx, n, k, cs, ns):
     """The proxy read path on received chunk frames (pageable message buffers,
-    one per chunk): gather the k surviving chunks of every stripe into the
-    device batch, full-output decode of 4 erasures, scatter the k data chunks
-    into per-chunk host frames.  `readers` concurrent callers (one context
-    each, like concurrent proxy requests) split the stripes.  User-data GiB/s."""
-    import threading
-
+    one per chunk, io.cc:209-216): the k surviving chunks of every stripe
+    gathered into HBM, full-output decode of n-k erasures (chunk_manager.cc:
+    738-800), the k data chunks scattered into per-chunk host frames.
+    `pipelined`: one nxec_decode_frames call (gather of batch b + 1, decode of
+    b, scatter of b - 1 at once); `sequential`: the same three steps one after
+    the other (nxec_gather_chunks x k, nxec_rs_decode_stripes,
+    nxec_scatter_chunks); `gather_only` / `scatter_only`: the two PCIe legs
+    alone, to name the limit.  User-data GiB/s (k*cs per stripe)."""
     import numpy as np
 
     failed = list(range(k - (n - k), k))  # worst case: n-k data chunks lost
     alive = [c for c in range(n) if c not in failed]
-    rx = np.random.default_rng(2).integers(0, 256, size=ns * k * cs, dtype=np.uint8)
+    rx = np.random.default_rng(2).integers(0, 256, size=ns * n * cs, dtype=np.uint8)
     tx = np.empty(ns * k * cs, dtype=np.uint8)
-    parts = []
-    for r in range(readers):
-        lo, hi = ns * r // readers, ns * (r + 1) // readers
-        c = ctx if r == 0 else nxec.Context(ctx.device)
-        st, dec = nxec.DeviceBuffer((hi - lo) * n * cs), nxec.DeviceBuffer((hi - lo) * k * cs)
-        rxf = {c_: [rx.ctypes.data + (s * k + i) * cs for s in range(lo, hi)] for i, c_ in enumerate(alive)}
-        txf = [tx.ctypes.data + i * cs for i in range(lo * k, hi * k)]
-        parts.append((c, st, dec, rxf, txf, hi - lo))
+    st, dec = nxec.DeviceBuffer(ns * n * cs), nxec.DeviceBuffer(ns * k * cs)
+    in_frames = [rx.ctypes.data + (s * n + c) * cs for s in range(ns) for c in range(n)]
+    out_frames = [tx.ctypes.data + i * cs for i in range(ns * k)]
+    rxf = {c: [in_frames[s * n + c] for s in range(ns)] for c in alive}
 
-    def once(part):
-        c, st, dec, rxf, txf, m = part
+    def gather():
         for cid in alive:
-            c.gather_chunks(rxf[cid], cs, st.ptr + cid * cs, n * cs)
-        c.rs_decode(n, k, failed, st.ptr, cs, n * cs, dec.ptr, cs, k * cs, cs, m)
-        c.scatter_chunks(dec.ptr, cs, txf, cs)
+            ctx.gather_chunks(rxf[cid], cs, st.ptr + cid * cs, n * cs)
 
-    def run_all(reps):
-        th = [threading.Thread(target=lambda p=p: [once(p) for _ in range(reps)]) for p in parts]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
+    def scatter():
+        ctx.scatter_chunks(dec.ptr, cs, out_frames, cs)
 
-    run_all(1)
-    reps = 3
-    t0 = time.perf_counter()
-    run_all(reps)
-    dt = (time.perf_counter() - t0) / reps
-    for c, st, dec, _, _, _ in parts:
-        st.free()
-        dec.free()
-        if c is not ctx:
-            c.close()
-    return ns * k * cs / dt / GIB
+    def sequential():
+        gather()
+        ctx.rs_decode(n, k, failed, st.ptr, cs, n * cs, dec.ptr, cs, k * cs, cs, ns)
+        scatter()
+
+    def pipelined():
+        ctx.decode_frames(n, k, failed, in_frames, out_frames, cs, ns)
+
+    def rate(fn, reps=3):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        ctx.sync()
+        return round(ns * k * cs / ((time.perf_counter() - t0) / reps) / GIB, 2)
+
+    out = {"pipelined": rate(pipelined), "sequential": rate(sequential), "gather_only": rate(gather),
+           "scatter_only": rate(scatter), "stripes": ns, "erasures": failed}
+    # the pipelined call wrote the original data chunks (parity-free check: the
+    # survivors were random, so compare against the sequential path's output)
+    want = tx.copy()
+    pipelined()
+    out["pipelined_equals_sequential"] = bool(np.array_equal(tx, want))
+    st.free()
+    dec.free()
+    return out
 
 
 def recover_frames_rate(ctx, n, k, cs, ns):

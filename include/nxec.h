@@ -217,6 +217,21 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  *  - otherwise the packed layout (chunk_stride = len rounded up to 16,
  *    stripe_stride = n * chunk_stride). */
 #define NXEC_LAYOUT_RECOVER_HEAVY 1
+
+/* The same choice measured on this device instead of read from the table
+ * above: how DRAM channels and banks serve the k + rows streams of a column
+ * depends on the chunk and stripe strides in ways no static rule captures
+ * for every geometry (a 4 KiB chunk pad is worth +0.02 of 8
+ * TB/s for RS(16,4) 256 KiB chunks and costs -0.11 at 1 MiB).  Times RS(n,k)
+ * encode -- and, with NXEC_LAYOUT_RECOVER_HEAVY, a scattered n-k erasure
+ * recover -- over a scratch batch of about budget_bytes (<= 0: 24 GiB, capped
+ * at a quarter of the free device memory) for a few candidate layouts (the
+ * table's, packed, chunk pads of 2, 4 and 8 KiB, an odd stripe stride) and
+ * returns the fastest.  The result is cached per (device, n, k, len, flags);
+ * the first call for a shape takes ~0.1-0.3 s.  Uses ctx's stream and
+ * device; the scratch batch is freed before it returns. */
+int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
+                            int64_t *chunk_stride, int64_t *stripe_stride);
 int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride);
 
 /* Host-resident batch encode (the proxy write path): h_data [s][k][len] in,
@@ -384,8 +399,11 @@ int nxec_encode_objects(nxec_ctx_t *ctx, int n, int k, int nobjects, const unsig
  * slot (same layout as above), and chunks past it are all zero bytes.
  * Parity and digests are those of the zero-padded stripe, as without the
  * flag; tail-arena slots of whole and all-zero chunks are left unspecified
- * (the one-launch path leaves them alone: k_files_md5 then writes ~1/k of
- * the tail bytes). */
+ * (the one-launch path reads the last stripe in place and writes only the
+ * partial chunk's slot -- one chunk of k -- except for an object that ends
+ * within 16 bytes of a 4 KiB page boundary with a chunk length that is not
+ * a multiple of 16, whose chunks from the one that would read past the
+ * page are copied zero padded to their slots first). */
 #define NXEC_OBJECTS_TAIL_INPLACE 1
 /* NXEC_OBJECTS_ASYNC: return once the work is queued on `stream` (NULL: the
  * context's) instead of when it is done.  lengths[] and d_objects[] (host
@@ -491,6 +509,21 @@ int nxec_request_wait(nxec_request_t *req);
  * Synchronous. */
 int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
                            unsigned char *const *frames, int64_t len, int64_t nstripes);
+
+/* The proxy's read path on received frames, pipelined inside one call:
+ * decodeFile (chunk_manager.cc:738-800, RSCode::decode's all-k output,
+ * rs.cc:111-236) for a batch of stripes whose chunks arrived as frames
+ * (io.cc:209-216).  in_frames[s*n + c] is chunk c of stripe s (len bytes, any
+ * alignment, pageable or pinned); only the k chunks rs.cc:252-265 chooses are
+ * read (entries of failed chunks may be NULL).  All k data chunks of stripe s
+ * are written to out_frames[s*k + j].  The stripes go through HBM in batches
+ * of batch_stripes (<= 0: about 64 MiB of chunks per batch) on three streams:
+ * the gather of batch b + 1 (host -> device), the decode of batch b and the
+ * scatter of batch b - 1 (device -> host) run at once, so both PCIe
+ * directions and the host copy pool are busy together.  Synchronous. */
+int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                       const unsigned char *const *in_frames, unsigned char *const *out_frames, int64_t len,
+                       int64_t nstripes, int64_t batch_stripes);
 
 /* ---- Multi-GPU group in one process: one context per device,
  * a batch's stripes split into contiguous ranges (sizes differ by at most one),
@@ -600,11 +633,13 @@ int nxec_host_range_mapped(const void *p, size_t bytes);
  *     length), together with a 64-bit fingerprint of the bytes: a take is a hit
  *     only on the noting thread, for the same length, and while the bytes
  *     still have that fingerprint (a buffer freed with plain free() and handed
- *     out again, or rewritten, is hashed afresh).  Each noting call clears the
- *     thread's entries first; an entry is taken once; nxec_digest_forget (any
- *     thread; Chunk::release calls it) drops the buffer's entry.  The marks
- *     RSCode::encode leaves on Chunks hold while the thread's digest epoch is
- *     unchanged: Chunk::allocateData and every freed Chunk buffer move it on.
+ *     out again, or rewritten, is hashed afresh).  Each coding call clears the
+ *     thread's entries first (nxec_digest_clear), a thread's entries go when
+ *     it exits; an entry is taken once; nxec_digest_forget (any thread;
+ *     Chunk::release calls it) drops the buffer's entry.  The marks
+ *     RSCode::encode leaves on Chunks hold only on the marking thread and
+ *     while its digest epoch is unchanged: Chunk::allocateData and every freed
+ *     Chunk buffer move it on, to a value no thread has held before.
  *     nxec_chunk_md5_mode: NXEC_CHUNK_MD5 = 0 (never; computeMD5 hashes on the
  *     host), 1 (default: RSCode::encode, whose n digests per stripe the GPU
  *     finishes sooner than one host thread hashing them in turn), 2 (also the

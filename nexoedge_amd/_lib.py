@@ -85,6 +85,8 @@ _PROTOS = {
     "nxec_gather_chunks": (C.c_int, [vp, vp, i64, i64, vp, i64, vp]),
     "nxec_scatter_chunks": (C.c_int, [vp, vp, i64, i64, i64, vp, vp]),
     "nxec_rs_recover_frames": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64]),
+    "nxec_batch_layout_tuned": (C.c_int, [vp, C.c_int, C.c_int, i64, C.c_int, i64, C.POINTER(i64), C.POINTER(i64)]),
+    "nxec_decode_frames": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp, i64, i64, i64]),
     "nxec_gather_chunks_async": (C.c_int, [vp, vp, i64, i64, vp, i64, vp, C.POINTER(vp)]),
     "nxec_scatter_chunks_async": (C.c_int, [vp, vp, i64, i64, i64, vp, vp, C.POINTER(vp)]),
     "nxec_request_wait": (C.c_int, [vp]),

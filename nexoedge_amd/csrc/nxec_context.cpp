@@ -72,19 +72,20 @@ class HostPool {
     return pool;
   }
   // runs fn(i) for i in [0, n), returns when all are done.  The pool serves
-  // one job at a time: a caller arriving while it is busy (many concurrent
+  // two jobs at a time (a pipelined caller's gather and scatter,
+  // nxec_decode_frames); a caller arriving while both run (many concurrent
   // callers already keep the cores busy) runs its items inline.
   void parallel_for(int n, const std::function<void(int)> &fn) {
     if (n <= 0) return;
-    bool expected = false;
-    if (n == 1 || workers_.empty() || !busy_.compare_exchange_strong(expected, true)) {
+    if (n == 1 || workers_.empty() || jobs_.fetch_add(1) >= kJobs) {
+      if (n > 1 && !workers_.empty()) jobs_.fetch_sub(1);
       for (int i = 0; i < n; i++) fn(i);
       return;
     }
     struct Release {
-      std::atomic<bool> &b;
-      ~Release() { b.store(false); }
-    } release{busy_};
+      std::atomic<int> &j;
+      ~Release() { j.fetch_sub(1); }
+    } release{jobs_};
     struct Job {
       const std::function<void(int)> *fn;
       std::atomic<int> next{0}, done{0};
@@ -141,18 +142,18 @@ class HostPool {
   std::condition_variable cv_;
   std::deque<std::function<void()>> tasks_;
   std::vector<std::thread> workers_;
-  std::atomic<bool> busy_{false};
+  static constexpr int kJobs = 2;
+  std::atomic<int> jobs_{0};
   bool stop_ = false;
 };
 
 }  // namespace
 
 bool host_direct_enabled() {
-  static const bool on = [] {  // deployment setting NXEC_HOST_DIRECT
-    const char *e = std::getenv("NXEC_HOST_DIRECT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  // deployment setting NXEC_HOST_DIRECT, read at every call:
+  // a host may switch zero copy off and on between calls (bench.py times both)
+  const char *e = std::getenv("NXEC_HOST_DIRECT");
+  return !(e && e[0] == '0');
 }
 
 bool test_fault(const char *name) {
@@ -243,20 +244,22 @@ int ensure_device(int device) {
   return NXEC_OK;
 }
 
-int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out) {
+int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out, bool may_wait) {
   Slot *s = nullptr;
   {
     // best fit: the smallest free slot that holds `bytes`, else the largest
     // (grown below) -- so callers of different sizes do not keep re-pinning
-    // each other's slots (hipHostMalloc of a GiB costs ~0.1 s)
-    // (slots still read by an asynchronous call's launches only when no idle
-    // one is free and the context already has kAsyncSlots: then the best of
-    // those, waited on below)
+    // each other's slots (hipHostMalloc of a GiB costs ~0.1 s).  Slots still
+    // read by an asynchronous call's launches are taken only by an
+    // asynchronous caller (may_wait), only when no idle one is free and the
+    // context already has kAsyncSlots: the best of those, waited on below.
+    // Everyone else gets an idle slot or a new one (never a wait on another
+    // stream's queued work).
     std::lock_guard<std::mutex> lk(ctx->slot_mu);
     int best = -1;
     bool any_idle = false;
     for (Slot *f : ctx->free_slots) any_idle = any_idle || f->idle();
-    const bool only_idle = any_idle || ctx->all_slots.size() < kAsyncSlots;
+    const bool only_idle = !may_wait || any_idle || ctx->all_slots.size() < kAsyncSlots;
     for (int i = 0; i < static_cast<int>(ctx->free_slots.size()); i++) {
       if (only_idle && !ctx->free_slots[i]->idle()) continue;
       const size_t c = ctx->free_slots[i]->cap;

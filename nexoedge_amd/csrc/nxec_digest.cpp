@@ -24,12 +24,16 @@
 //    recycled or rewritten buffer is hashed afresh instead of inheriting a
 //    stale digest.  The fingerprint reads the region once on the host (~10+
 //    GB/s per thread against OpenSSL MD5's ~0.6 GB/s).  The table is global
-//    under a mutex: nxec_digest_forget from any thread drops an entry, and a
-//    noting call clears the calling thread's older entries first.
+//    under a mutex and keyed by address (note, take and forget are O(1)):
+//    nxec_digest_forget from any thread drops an entry, nxec_digest_clear
+//    drops the calling thread's, and a thread's entries go when it exits.
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
+#include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "nxec.h"
@@ -39,7 +43,7 @@ namespace {
 
 struct Entry {
   uint64_t owner;
-  const void *p;
+  uint64_t serial;  // when it was noted (FIFO eviction)
   int64_t len;
   uint64_t fp;
   unsigned char md5[16];
@@ -47,18 +51,47 @@ struct Entry {
 
 constexpr size_t kMaxEntries = 4096;
 
+// The table, keyed by buffer address: note / take / forget are O(1); `order`
+// keeps (address, serial) in noting order for the FIFO bound (stale pairs of
+// entries already taken or replaced are skipped when met).
 std::mutex g_mu;
-std::vector<Entry> g_table;
+std::unordered_map<const void *, Entry> g_table;
+std::deque<std::pair<const void *, uint64_t>> g_order;
+uint64_t g_serial = 0;
 std::atomic<uint64_t> g_next_owner{1};
 std::atomic<size_t> g_count{0};  // entries in g_table (lets forget skip the lock when empty)
+// Chunk digest epochs: drawn from one counter, so no two threads (and no
+// two moments of one thread) ever hold the same value
+std::atomic<uint64_t> g_epoch{1};
 
-uint64_t self() {
-  thread_local const uint64_t id = g_next_owner.fetch_add(1, std::memory_order_relaxed);
-  return id;
+// drops the entries `owner` noted (the thread's own, listed in `mine`)
+void drop_owner(uint64_t owner, std::vector<const void *> &mine) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (const void *p : mine) {
+    auto it = g_table.find(p);
+    if (it != g_table.end() && it->second.owner == owner) g_table.erase(it);
+  }
+  mine.clear();
+  g_count.store(g_table.size(), std::memory_order_relaxed);
+}
+
+// The calling thread's identity and the buffers it noted; a thread that exits
+// (the reference runs a thread per request) takes its entries with it.
+struct Self {
+  uint64_t id = g_next_owner.fetch_add(1, std::memory_order_relaxed);
+  std::vector<const void *> noted;
+  ~Self() {
+    if (!noted.empty()) drop_owner(id, noted);
+  }
+};
+
+Self &self() {
+  thread_local Self s;
+  return s;
 }
 
 uint64_t &epoch() {
-  thread_local uint64_t e = 1;
+  thread_local uint64_t e = g_epoch.fetch_add(1, std::memory_order_relaxed);
   return e;
 }
 
@@ -111,49 +144,57 @@ int nxec_chunk_md5_mode(void) {
   return mode;
 }
 
+// A Chunk's mark (chunk.hh) is valid only on the thread that set it and only
+// until that thread's epoch moves: a fresh epoch comes from the global counter.
 uint64_t nxec_digest_epoch(void) { return epoch(); }
-void nxec_digest_epoch_bump(void) { ++epoch(); }
+void nxec_digest_epoch_bump(void) { epoch() = g_epoch.fetch_add(1, std::memory_order_relaxed); }
 
 void nxec_digest_clear(void) {
-  const uint64_t me = self();
-  std::lock_guard<std::mutex> g(g_mu);
-  size_t w = 0;
-  for (size_t i = 0; i < g_table.size(); i++)
-    if (g_table[i].owner != me) g_table[w++] = g_table[i];
-  g_table.resize(w);
-  g_count.store(w, std::memory_order_relaxed);
+  Self &me = self();
+  if (!me.noted.empty()) drop_owner(me.id, me.noted);
 }
 
 int nxec_digest_note(const void *p, int64_t len, const unsigned char *md5) {
   if (!p || len <= 0 || !md5) return NXEC_ERR_INVALID;
+  Self &me = self();
   Entry e;
-  e.owner = self();
-  e.p = p;
+  e.owner = me.id;
   e.len = len;
   e.fp = nxec::fingerprint64(p, len);  // outside the lock
   std::memcpy(e.md5, md5, 16);
   std::lock_guard<std::mutex> g(g_mu);
-  for (Entry &x : g_table)
-    if (x.p == p) {  // a newer digest for the same buffer replaces the old one, whoever noted it
-      x = e;
-      return NXEC_OK;
+  e.serial = ++g_serial;
+  // a newer digest for the same buffer replaces the old one, whoever noted it
+  g_table[p] = e;
+  g_order.emplace_back(p, e.serial);
+  me.noted.push_back(p);
+  while (g_table.size() > kMaxEntries && !g_order.empty()) {  // FIFO bound: the oldest live entry goes
+    const auto old = g_order.front();
+    g_order.pop_front();
+    auto it = g_table.find(old.first);
+    if (it != g_table.end() && it->second.serial == old.second) g_table.erase(it);
+  }
+  if (g_order.size() > 4 * kMaxEntries) {  // stale pairs (taken / replaced entries) pile up: compact
+    std::deque<std::pair<const void *, uint64_t>> live;
+    for (const auto &o : g_order) {
+      auto it = g_table.find(o.first);
+      if (it != g_table.end() && it->second.serial == o.second) live.push_back(o);
     }
-  if (g_table.size() >= kMaxEntries) g_table.erase(g_table.begin());
-  g_table.push_back(e);
+    g_order.swap(live);
+  }
   g_count.store(g_table.size(), std::memory_order_relaxed);
   return NXEC_OK;
 }
 
 int nxec_digest_take(const void *p, int64_t len, unsigned char *md5) {
-  const uint64_t me = self();
+  const uint64_t me = self().id;
   Entry e;
   {
     std::lock_guard<std::mutex> g(g_mu);
-    size_t i = 0;
-    while (i < g_table.size() && !(g_table[i].p == p && g_table[i].owner == me)) i++;
-    if (i == g_table.size()) return 0;
-    e = g_table[i];
-    g_table.erase(g_table.begin() + static_cast<long>(i));
+    auto it = g_table.find(p);
+    if (it == g_table.end() || it->second.owner != me) return 0;
+    e = it->second;
+    g_table.erase(it);
     g_count.store(g_table.size(), std::memory_order_relaxed);
   }
   // the bytes must still be the ones the digest was computed over
@@ -163,15 +204,10 @@ int nxec_digest_take(const void *p, int64_t len, unsigned char *md5) {
 }
 
 void nxec_digest_forget(const void *p) {
-  ++epoch();  // a Chunk buffer is going away: this thread's Chunk marks end here
+  nxec_digest_epoch_bump();  // a Chunk buffer is going away: this thread's Chunk marks end here
   if (g_count.load(std::memory_order_relaxed) == 0) return;  // a racing note is for a live buffer, not p
   std::lock_guard<std::mutex> g(g_mu);
-  for (size_t i = 0; i < g_table.size(); i++)
-    if (g_table[i].p == p) {
-      g_table.erase(g_table.begin() + static_cast<long>(i));
-      g_count.store(g_table.size(), std::memory_order_relaxed);
-      return;
-    }
+  if (g_table.erase(p)) g_count.store(g_table.size(), std::memory_order_relaxed);
 }
 
 }  // extern "C"

@@ -24,9 +24,12 @@ namespace {
 // steps in flight as k_mul_md5, as the 64-bit source pointers leave room (4
 // through k = 11, 3 through 14, then 2); the masked-chunk state takes one step
 // (3 and 4 steps measured the same in round 4), two from k = 13 (no spills)
+#ifndef NXEC_FM_MASK_DEPTH
+#define NXEC_FM_MASK_DEPTH 3  // design A/B: separate builds with -DNXEC_FM_MASK_DEPTH
+#endif
 template <int K, bool MASK>
 constexpr int fm_depth() {
-  constexpr int cap = !MASK ? 4 : K >= 13 ? 2 : 3;
+  constexpr int cap = !MASK ? 4 : K >= 13 ? 2 : NXEC_FM_MASK_DEPTH;
   return gm_depth<K>() > cap ? cap : gm_depth<K>();
 }
 
@@ -137,10 +140,6 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     // MASK: the load cursor's masked chunk (K: none) and its bytes in the object
     int lj = K;
     int32_t lvm = 0;
-    // a straddling vector read byte by byte, for the compute step sv_step
-    u32x4 sv = u32x4{0u, 0u, 0u, 0u};
-    int sv_step = -1, sv_j = K;
-    int lsteps = 0;  // load() calls so far: the workgroup step the next load feeds
     // source pointers of the lane's column: a request's chunks, or -- a lane
     // whose column holds no byte of the request (chunks under 256 bytes) --
     // the scratch line: nothing past a chunk's 16-byte padding is read
@@ -156,20 +155,24 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     set_src(0, tmax_of(len0) >= 0);
     auto load = [&](u32x4(&d)[K]) {
       const int64_t off = static_cast<int64_t>(min(lt, ltcl)) * kEncMd5Step;
-      // MASK events of this lane's vector of chunk lj: it straddles the
-      // object's end (st), or lies past it / repeats a step (zr: from now on
-      // the chunk reads the zero line)
-      bool st = false, zr = false;
       if (MASK) {
-        const int32_t co = static_cast<int32_t>(off) + v * 16;
-        st = lj < K && co < lvm && co + 16 > lvm && lt <= ltcl;
-        zr = lj < K && (co >= lvm || lt > ltcl);
+        // this lane's vector of chunk lj reaches the object's end: from this
+        // step on the chunk reads the zero line (the vector across the end
+        // gets its bytes from the compute step).  A rare, wave-uniform branch:
+        // the step's loads below stay the plain kernel's.
+        const bool ev = lj < K && static_cast<int32_t>(off) + v * 16 + 16 > lvm;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
+          if (ev) {
+#pragma unroll
+            for (int j = 0; j < K; j++)
+              if (j == lj) sp[j] = a.zero + v * 16;
+            lj = K;
+          }
+        }
       }
-      const bool wev = MASK && __builtin_amdgcn_ballot_w64(st || zr) != 0;  // wave-uniform
 #pragma unroll
       for (int j = 0; j < K; j++) {
         const uint8_t *pj = sp[j] + off;
-        if (wev && (st || zr) && j == lj) pj = a.zero + v * 16 + off;
         // plain (cached) loads: a chunk that is not 128-byte aligned (an
         // object at any 16-byte offset, a last stripe at any byte) shares its
         // boundary lines between consecutive steps; streaming loads fetched
@@ -182,27 +185,6 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         else
           d[j] = dev::ld_global_stream(pj);
       }
-      if (wev) {
-        if (st) {  // the valid bytes only, zero padded (the reference's padding, chunk_manager.cc:390-399)
-          const uint8_t *pb = nullptr;
-#pragma unroll
-          for (int j = 0; j < K; j++)
-            if (j == lj) pb = sp[j] + off;
-          const int nb = lvm - (static_cast<int32_t>(off) + v * 16);
-          uint32_t w[4] = {0u, 0u, 0u, 0u};
-          for (int b = 0; b < nb; b++) w[b >> 2] |= static_cast<uint32_t>(pb[b]) << (8 * (b & 3));
-          sv = u32x4{w[0], w[1], w[2], w[3]};
-          sv_step = lsteps;
-          sv_j = lj;
-        }
-        if (zr) {
-#pragma unroll
-          for (int j = 0; j < K; j++)
-            if (j == lj) sp[j] = a.zero + v * 16;
-          lj = K;
-        }
-      }
-      lsteps++;
       if (++lt == lT) {
         if (lr + 1 < cnt) {  // next request of the slot (pointers from the LDS table)
           lr++;
@@ -235,24 +217,46 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     uint8_t *std_ = nullptr;
     int64_t scls = 0;
     int32_t sj0 = 0, sjm = -1, scl = 0;
+    // MASK: the compute request's masked chunk (K: none) and its bytes in the object
+    int cj = K;
+    int32_t cvm = 0;
     auto set_store = [&](int li) {
       if (!TSTORE && !MASK) return;
       std_ = act ? reinterpret_cast<uint8_t *>(q[li * rec + K + a.p + 2]) : nullptr;
       scls = static_cast<int64_t>(q[li * rec + K + a.p + 3] & 0xffffffffu);
+      cvm = static_cast<int32_t>(q[li * rec + K + a.p + 3] >> 32);
       const uint64_t m = q[li * rec + K + a.p + 4];
       sj0 = static_cast<int32_t>((m >> 8) & 0xff);
+      cj = act ? static_cast<int>(m & 0xff) : K;
       sjm = (m >> 16) & 1 ? static_cast<int32_t>(m & 0xff) : -1;
       scl = static_cast<int32_t>(len_of(li));
     };
     set_store(0);
-    auto run = [&](int step, const u32x4(&d)[K]) {
+    auto run = [&](int step, u32x4(&d)[K]) {
       const bool ok = live && ct <= ctmax;
       // wave-uniform: only waves holding a last stripe store, only steps with a straddling vector patch
       const bool wst = TSTORE && __builtin_amdgcn_ballot_w64(ok && std_ != nullptr) != 0;
-      const bool hit = MASK && sv_step == step;
-      const bool wsv = MASK && __builtin_amdgcn_ballot_w64(hit) != 0;
       uint8_t *rb = row + (step & 1) * buf_bytes;
       const int32_t pos = ct * kEncMd5Step + v * 16;
+      // MASK: this lane's vector of chunk cj straddles the object's end (it was
+      // loaded as zeros): read its valid bytes one by one -- nothing past the
+      // object's last byte -- zero padded (the reference's padding,
+      // chunk_manager.cc:390-399)
+      if (MASK) {
+        const bool hit = ok && cj < K && pos < cvm && pos + 16 > cvm;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(hit) != 0, 0)) {
+          u32x4 sv = u32x4{0u, 0u, 0u, 0u};
+          if (hit) {
+            const uint8_t *pb = reinterpret_cast<const uint8_t *>(q[cr * rec + cj]) + pos;
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int b = 0; b < cvm - pos; b++) w[b >> 2] |= static_cast<uint32_t>(pb[b]) << (8 * (b & 3));
+            sv = u32x4{w[0], w[1], w[2], w[3]};
+          }
+#pragma unroll
+          for (int j = 0; j < K; j++)
+            if (hit && j == cj) d[j] = sv;
+        }
+      }
       uint32_t acc[16];
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = 0;
@@ -260,10 +264,6 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       for (int j = 0; j < K; j += 2) {
         const int j1 = j + 1 < K ? j + 1 : j;
         u32x4 x0 = d[j], x1 = d[j1];
-        if (wsv) {  // the straddling vector was loaded as zeros: put its bytes in
-          if (hit && sv_j == j) x0 = sv;
-          if (hit && sv_j == j1) x1 = sv;
-        }
         if (ok) {  // past a request's end its row is left as is: the hash lanes mask it
           *reinterpret_cast<u32x4 *>(rb + j * kEmRow) = x0;
           if (j + 1 < K) *reinterpret_cast<u32x4 *>(rb + (j + 1) * kEmRow) = x1;

@@ -4,6 +4,8 @@
 // (io.cc:209-216, :334-336), its asynchronous forms, the recover straight
 // into frames, and the host-inclusive object write.
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <cstring>
 #include <functional>
 #include <new>
@@ -393,6 +395,128 @@ int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
   if (!rc) rc = hip_check(he, "recover_frames sync");
   if (!lk.owns_lock()) priv.release();
   return rc;
+}
+
+int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int nfailed,
+                       const unsigned char *const *in_frames, unsigned char *const *out_frames, int64_t len,
+                       int64_t nstripes, int64_t batch_stripes) {
+  if (!ctx || !valid_nk(n, k) || nfailed < 0 || (nfailed > 0 && !failed) || len < 0 || nstripes < 0 ||
+      (nstripes > 0 && (!in_frames || !out_frames)))
+    return set_error(NXEC_ERR_INVALID, "nxec_decode_frames: invalid arguments");
+  if (len == 0 || nstripes == 0) return NXEC_OK;
+  std::vector<int32_t> inputs(n);
+  int ni = 0, mi = 0;
+  int rc = nxec_rs_plan(n, k, failed, nfailed, 0, inputs.data(), &ni, &mi, nullptr);  // rs.cc:252-265
+  if (rc) return rc;
+  for (int64_t s = 0; s < nstripes; s++) {
+    for (int j = 0; j < k; j++)
+      if (!in_frames[s * n + inputs[j]] || !out_frames[s * k + j])
+        return set_error(NXEC_ERR_INVALID, "nxec_decode_frames: stripe %lld: null frame", static_cast<long long>(s));
+  }
+  if ((rc = ensure_device(ctx->device))) return rc;
+  // staging rows: the k chosen inputs [B][k][stride], then all k data chunks [B][k][stride]
+  // (erased data chunks get inverse rows, rs.cc:196,228-230; surviving ones
+  // are unit rows, i.e. copies of their input)
+  std::vector<int32_t> targets, src(k), copy(k, -1);
+  for (int i = 0; i < nfailed; i++)
+    if (failed[i] < k) targets.push_back(failed[i]);
+  for (int j = 0; j < k; j++) {
+    src[j] = j;
+    if (inputs[j] < k) copy[j] = inputs[j];
+  }
+  std::vector<uint8_t> dm(std::max<size_t>(1, targets.size() * size_t(k)));
+  if (!targets.empty() &&
+      (rc = nxec_rs_decode_matrix(n, k, inputs.data(), targets.data(), static_cast<int>(targets.size()), dm.data())))
+    return rc;
+  const int64_t stride = (len + 15) / 16 * 16;
+  int64_t B = batch_stripes > 0 ? batch_stripes : std::max<int64_t>(1, (int64_t(64) << 20) / (int64_t(k) * stride));
+  B = std::min(B, nstripes);
+  const int64_t nb = (nstripes + B - 1) / B;
+  std::unique_lock<std::mutex> lk;
+  ObjStage priv, *pstg = nullptr;
+  if ((rc = batch_stage(ctx, size_t(B) * 2 * k * stride, lk, priv, &pstg))) return rc;
+  ObjStage &stg = *pstg;
+  // batch b lives in staging slot b % kObjSlots; one stream per stage
+  hipStream_t s_gather = stg.streams[0], s_decode = stg.streams[1], s_scatter = stg.streams[2];
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t gathered = 0, decoded = 0, scattered = 0;  // batches done per stage
+  int err = NXEC_OK;
+  std::string err_msg;
+  auto fail = [&](int code) {  // the first error wins; every stage stops
+    std::lock_guard<std::mutex> g(mu);
+    if (!err) {
+      err = code;
+      err_msg = last_error();
+    }
+    cv.notify_all();
+  };
+  auto wait_for = [&](const int64_t &counter, int64_t want) {
+    std::unique_lock<std::mutex> g(mu);
+    cv.wait(g, [&] { return err != NXEC_OK || counter >= want; });
+    return err == NXEC_OK;
+  };
+  auto done = [&](int64_t &counter) {
+    std::lock_guard<std::mutex> g(mu);
+    counter++;
+    cv.notify_all();
+  };
+  auto in_rows = [&](int64_t b) { return stg.d + (b % kObjSlots) * stg.cap; };
+  auto out_rows = [&](int64_t b) { return in_rows(b) + size_t(B) * k * stride; };
+  auto run_stage = [&](auto &&body) {
+    return std::thread([&, body]() mutable {
+      try {
+        body();
+      } catch (const std::exception &e) {
+        fail(set_error(NXEC_ERR_NOMEM, "nxec_decode_frames: %s", e.what()));
+      }
+    });
+  };
+  std::thread gatherer = run_stage([&]() {
+    std::vector<const unsigned char *> fr(static_cast<size_t>(B));
+    for (int64_t b = 0; b < nb; b++) {
+      if (b >= kObjSlots && !wait_for(scattered, b - kObjSlots + 1)) return;  // the slot's previous batch has left
+      const int64_t s0 = b * B, m = std::min(B, nstripes - s0);
+      for (int j = 0; j < k; j++) {
+        for (int64_t i = 0; i < m; i++) fr[size_t(i)] = in_frames[(s0 + i) * n + inputs[j]];
+        if (int r = nxec_gather_chunks(ctx, fr.data(), m, len, in_rows(b) + j * stride, int64_t(k) * stride, s_gather))
+          return fail(r);
+      }
+      done(gathered);
+    }
+  });
+  std::thread scatterer = run_stage([&]() {
+    std::vector<unsigned char *> fr(static_cast<size_t>(B));
+    for (int64_t b = 0; b < nb; b++) {
+      if (!wait_for(decoded, b + 1)) return;
+      const int64_t s0 = b * B, m = std::min(B, nstripes - s0);
+      for (int j = 0; j < k; j++) {
+        for (int64_t i = 0; i < m; i++) fr[size_t(i)] = out_frames[(s0 + i) * k + j];
+        if (int r = nxec_scatter_chunks(ctx, out_rows(b) + j * stride, int64_t(k) * stride, m, len, fr.data(), s_scatter))
+          return fail(r);
+      }
+      done(scattered);
+    }
+  });
+  for (int64_t b = 0; b < nb; b++) {  // decode on the calling thread
+    if (!wait_for(gathered, b + 1)) break;
+    const int64_t m = std::min(B, nstripes - b * B);
+    int r = stripes_mul_impl(ctx, static_cast<int>(targets.size()), k, dm.data(), in_rows(b), nullptr, src.data(), stride,
+                             int64_t(k) * stride, out_rows(b), nullptr, targets.data(), stride, int64_t(k) * stride,
+                             copy.data(), len, m, s_decode);
+    if (!r) r = hip_check(hipStreamSynchronize(s_decode), "decode_frames sync");
+    if (r) {
+      fail(r);
+      break;
+    }
+    done(decoded);
+  }
+  gatherer.join();
+  scatterer.join();
+  for (int i = 0; i < kObjSlots; i++) (void)hipStreamSynchronize(stg.streams[i]);
+  if (!lk.owns_lock()) priv.release();
+  if (err) restore_error(err_msg);
+  return err;
 }
 
 int nxec_encode_object_host(nxec_ctx_t *ctx, int n, int k, const unsigned char *h_object, int64_t length,

@@ -245,8 +245,11 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
           const int64_t pend = static_cast<int64_t>(((end + 4095) & ~uintptr_t(4095)) - reinterpret_cast<uintptr_t>(tb));
           const int64_t jov = pend >= cls ? (pend - cls) / cl + 1 : 0;  // first chunk that would leave the page
           int64_t j0 = k, jm = k;
-          if (jov < jf) {
-            j0 = jov;
+          if (jov < jf || !tuning().files_fold) {
+            // (the fold probe off: round 4's in-place rule, the chunks from the partial one -- or
+            // the first that would read past the object's last 16-byte line -- through the pad copy)
+            const int64_t line = static_cast<int64_t>(((end + 15) & ~uintptr_t(15)) - reinterpret_cast<uintptr_t>(tb));
+            j0 = tuning().files_fold ? jov : std::min(jf, line >= cls ? (line - cls) / cl + 1 : 0);
             for (int j = 0; j < k; j++) q_src.push_back(j < j0 ? tb + j * cl : td + j * cls);
             pads.push_back({tb + j0 * cl, td + j0 * cls, rem - j0 * cl, cl, cls, k - j0});
             pad_bstart.push_back(static_cast<uint32_t>(pad_blocks));
@@ -350,7 +353,7 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   size_t off[kTabs + 1] = {0};
   for (int i = 0; i < kTabs; i++) off[i + 1] = off[i] + (tabs[i].bytes + 15) / 16 * 16;
   Slot *slot = nullptr;
-  rc = acquire_slot(ctx, std::max<size_t>(off[kTabs], 16), &slot);
+  rc = acquire_slot(ctx, std::max<size_t>(off[kTabs], 16), &slot, async);
   if (rc) return rc;
   // the slot's staging may still be in use by an earlier call on its own stream
   rc = hip_check(hipStreamSynchronize(slot->stream), "slot sync");

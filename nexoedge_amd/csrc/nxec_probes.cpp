@@ -28,8 +28,7 @@ Tuning read_tuning() {
   if ((e = knob("NXEC_FM_PROBE"))) t.fm_probe = std::atoi(e);
   if ((e = knob("NXEC_FILES_PACK"))) t.files_pack = e[0] != '0';
   if ((e = knob("NXEC_FILES_LOADS"))) t.files_cached_loads = e[0] != '0';
-  if ((e = knob("NXEC_FILES_CLOCK"))) t.files_clock = e[0] == '1';
-  if ((e = knob("NXEC_TIMING"))) t.timing = e[0] == '1';
+  if ((e = knob("NXEC_FILES_FOLD"))) t.files_fold = e[0] != '0';
   if ((e = knob("NXEC_MD5_CFG"))) {
     int d = 2, g = 8, nt = 0;
     if (std::sscanf(e, "%d,%d,%d", &d, &g, &nt) >= 2) t.md5_depth = d, t.md5_group = g, t.md5_nt = nt != 0;

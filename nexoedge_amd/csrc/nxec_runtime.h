@@ -145,9 +145,11 @@ struct nxec_ctx {
 namespace nxec {
 
 int ensure_device(int device);
-// A slot of at least `bytes` from the context's pool (best fit), waiting for
-// an asynchronous call's launches when it was handed back busy.
-int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out);
+// A slot of at least `bytes` from the context's pool (best fit).  Slots an
+// asynchronous call handed back busy go only to callers that may wait for
+// them (may_wait: the asynchronous multi-file write, once the context holds
+// kAsyncSlots); others get an idle slot or a new one.
+int acquire_slot(nxec_ctx_t *ctx, size_t bytes, Slot **out, bool may_wait = false);
 void release_slot(nxec_ctx_t *ctx, Slot *s);
 // The context's persistent batch staging (kObjSlots slots of at least
 // slot_bytes), or a private one in `priv` while another call holds the

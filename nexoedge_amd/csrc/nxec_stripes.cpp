@@ -5,6 +5,9 @@
 // and the recommended batch layout.
 #include <algorithm>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "nxec_runtime.h"
@@ -378,6 +381,105 @@ int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int6
   }
   *chunk_stride = cs;
   *stripe_stride = ss;
+  return NXEC_OK;
+}
+
+namespace {
+std::mutex g_tuned_mu;
+std::map<std::tuple<int, int, int, int64_t, int>, std::pair<int64_t, int64_t>> g_tuned;
+}  // namespace
+
+int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
+                            int64_t *chunk_stride, int64_t *stripe_stride) {
+  if (!ctx || !valid_nk(n, k) || n == k || len <= 0 || !chunk_stride || !stripe_stride)
+    return set_error(NXEC_ERR_INVALID, "nxec_batch_layout_tuned: invalid arguments");
+  const auto key = std::make_tuple(ctx->device, n, k, len, flags);
+  {
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    auto it = g_tuned.find(key);
+    if (it != g_tuned.end()) {
+      *chunk_stride = it->second.first;
+      *stripe_stride = it->second.second;
+      return NXEC_OK;
+    }
+  }
+  int rc = ensure_device(ctx->device);
+  if (rc) return rc;
+  int64_t c0 = 0, s0 = 0;
+  if ((rc = nxec_batch_layout(n, len, flags, &c0, &s0))) return rc;
+  const int64_t packed = (len + 15) / 16 * 16;
+  std::vector<std::pair<int64_t, int64_t>> cand = {{c0, s0}, {packed, n * packed}};
+  for (int64_t pad : {int64_t(2048), int64_t(4096), int64_t(8192)}) cand.emplace_back(packed + pad, n * (packed + pad));
+  cand.emplace_back(packed, (n + 1) * packed);  // an odd stripe stride in chunks
+  std::sort(cand.begin(), cand.end());
+  cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+  size_t free_b = 0, total_b = 0;
+  NXEC_HIP(hipMemGetInfo(&free_b, &total_b));
+  int64_t budget = budget_bytes > 0 ? budget_bytes : int64_t(24) << 30;
+  budget = std::min<int64_t>(budget, static_cast<int64_t>(free_b / 4));
+  int64_t max_ss = 0;
+  for (const auto &c : cand) max_ss = std::max(max_ss, c.second);
+  if (budget < max_ss) budget = max_ss;
+  uint8_t *d = nullptr;
+  NXEC_HIP(hipMalloc(reinterpret_cast<void **>(&d), static_cast<size_t>(budget)));
+  hipStream_t st = ctx->stream;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  rc = hip_check(hipEventCreate(&e0), "hipEventCreate");
+  if (!rc) rc = hip_check(hipEventCreate(&e1), "hipEventCreate");
+  if (!rc) rc = launch_fill(d, static_cast<size_t>(budget), 0x7A11ull, st);
+  // a scattered recover (the slow patterns of DESIGN.md §3): the first
+  // min(n - k, 4) of chunks 1, 4, n - 3, n - 1 (the bench's {1,4,11,13} for RS(10,4))
+  std::vector<int32_t> scattered;
+  for (int32_t c : {1, 4, n - 3, n - 1})
+    if (static_cast<int>(scattered.size()) < std::min(n - k, 4) && c >= 0 && c < n &&
+        std::find(scattered.begin(), scattered.end(), c) == scattered.end())
+      scattered.push_back(c);
+  std::sort(scattered.begin(), scattered.end());
+  double best = -1;
+  std::pair<int64_t, int64_t> pick = {c0, s0};
+  for (const auto &c : cand) {
+    if (rc) break;
+    const int64_t ns = budget / c.second;
+    if (ns < 1) continue;
+    auto timed = [&](bool recover, double *ms) {
+      auto op = [&]() {
+        return recover ? nxec_rs_recover_stripes(ctx, n, k, scattered.data(), static_cast<int>(scattered.size()), d,
+                                                 c.first, c.second, len, ns, st)
+                       : nxec_rs_encode_stripes(ctx, n, k, d, c.first, c.second, len, ns, st);
+      };
+      int r = op();  // warm
+      if (!r) r = hip_check(hipEventRecord(e0, st), "hipEventRecord");
+      for (int i = 0; i < 3 && !r; i++) r = op();
+      if (!r) r = hip_check(hipEventRecord(e1, st), "hipEventRecord");
+      float t = 0;
+      if (!r) r = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+      if (!r) r = hip_check(hipEventElapsedTime(&t, e0, e1), "hipEventElapsedTime");
+      *ms = t / 3;
+      return r;
+    };
+    double ms_enc = 0, ms_rec = 0;
+    if ((rc = timed(false, &ms_enc))) break;
+    double rate = double(ns) * n * len / ms_enc;  // encode bytes: (k + p) * len per stripe
+    if (flags & NXEC_LAYOUT_RECOVER_HEAVY) {
+      if ((rc = timed(true, &ms_rec))) break;
+      rate = 0.5 * rate + 0.5 * double(ns) * (k + double(scattered.size())) * len / ms_rec;
+    }
+    if (rate > best * 1.002) {  // ties keep the earlier (smaller-stride) candidate
+      best = rate;
+      pick = c;
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(d);
+  if (rc) return rc;
+  {
+    std::lock_guard<std::mutex> lk(g_tuned_mu);
+    g_tuned[key] = pick;
+  }
+  *chunk_stride = pick.first;
+  *stripe_stride = pick.second;
   return NXEC_OK;
 }
 

@@ -27,8 +27,7 @@ struct Tuning {
   int fm_probe = -1;          // NXEC_FM_PROBE: k_files_md5 role probe (outputs invalid)
   bool files_pack = true;     // NXEC_FILES_PACK=0: one request per slot
   bool files_cached_loads = true;  // NXEC_FILES_LOADS=0: streaming loads in k_files_md5
-  bool files_clock = false;   // NXEC_FILES_CLOCK=1: per-workgroup timestamps on stderr
-  bool timing = false;        // NXEC_TIMING=1: host-side split of nxec_encode_objects_ex on stderr
+  bool files_fold = true;     // NXEC_FILES_FOLD=0: last stripes' partial chunks through the pad copy (round 4)
   int md5_depth = 2, md5_group = 8;  // NXEC_MD5_CFG=D,G[,NT]: k_md5 ring depth / blocks per group
   bool md5_nt = false;
   // host paths (nxec_agent.cpp, nxec_host_encode.cpp)

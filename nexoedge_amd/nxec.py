@@ -221,6 +221,12 @@ def device_info(dev: int = 0) -> dict:
     return {"arch": name.value.decode(), "cus": cus.value, "mem": mem.value}
 
 
+def set_device(dev: int) -> None:
+    """nxec_set_device: make `dev` the calling thread's current device (its
+    allocations, e.g. DeviceBuffer, land there)."""
+    check(lib.nxec_set_device(int(dev)), "nxec_set_device")
+
+
 def device_sync() -> None:
     check(lib.nxec_device_sync(), "nxec_device_sync")
 
@@ -582,6 +588,23 @@ class Context:
         check(lib.nxec_rs_recover_frames(C.c_void_p(self.ptr), n, k, fp, len(failed), tab, length, nstripes),
               "nxec_rs_recover_frames")
 
+    def batch_layout_tuned(self, n: int, k: int, length: int, flags: int = 0, budget_bytes: int = 0):
+        """nxec_batch_layout_tuned: (chunk_stride, stripe_stride) measured on this device."""
+        cs, ss = C.c_int64(), C.c_int64()
+        check(lib.nxec_batch_layout_tuned(C.c_void_p(self.ptr), n, k, length, flags, budget_bytes, C.byref(cs),
+                                          C.byref(ss)), "nxec_batch_layout_tuned")
+        return int(cs.value), int(ss.value)
+
+    def decode_frames(self, n: int, k: int, failed: Sequence[int], in_frames: Sequence[int],
+                      out_frames: Sequence[int], length: int, nstripes: int, batch_stripes: int = 0) -> None:
+        """nxec_decode_frames: in_frames = nstripes*n host addresses ([s][c]; 0 =
+        absent), out_frames = nstripes*k ([s][j]): the pipelined read path."""
+        f, fp = _i32(failed)
+        tin = (C.c_void_p * max(len(in_frames), 1))(*[int(x) if x else None for x in in_frames])
+        tout = (C.c_void_p * max(len(out_frames), 1))(*[int(x) if x else None for x in out_frames])
+        check(lib.nxec_decode_frames(C.c_void_p(self.ptr), n, k, fp, len(failed), tin, tout, length, nstripes,
+                                     batch_stripes), "nxec_decode_frames")
+
     def describe_launch(self, rows: int, k: int, length: int, nstripes: int) -> str:
         buf = C.create_string_buffer(512)
         check(lib.nxec_describe_launch(C.c_void_p(self.ptr), rows, k, length, nstripes, buf, 512), "describe")
@@ -644,6 +667,6 @@ class Group:
 
 __all__ = [
     "Group", "NxecError", "gf_mul", "gf_inv", "gen_rs_matrix", "invert_matrix", "init_tables", "rs_plan", "decode_matrix",
-    "encode_host", "ec_encode_data", "car_plan", "device_count", "device_info", "device_sync", "DeviceBuffer", "PinnedBuffer",
+    "encode_host", "ec_encode_data", "car_plan", "device_count", "device_info", "device_sync", "set_device", "DeviceBuffer", "PinnedBuffer",
     "Event", "Context",
 ]

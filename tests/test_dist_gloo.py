@@ -151,3 +151,19 @@ def test_bench_under_torch_distributed_run_world8():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 8 and d["ranks_seen"] == 8 and abs(d["max_elapsed_s"] - 0.008) < 1e-9
+
+
+def test_bench_group_flag_dry_run():
+    """`bench.py --gpus 8 --group` (the one-process nxec_group deployment
+    measured beside the ranks): the dry run rendezvouses the 8 ranks and rank 0
+    reports the group's plan -- 8 members, member i on device i, each with its
+    own stripe batch -- in the same single line."""
+    import json
+
+    r = _bench(["--gpus", "8", "--group", "--dry-run", "--stripes", "512", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["ranks_seen"] == 8
+    assert d["group"] == {"members": 8, "devices": list(range(8)), "stripes_per_member": 512}

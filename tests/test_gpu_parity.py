@@ -1106,6 +1106,34 @@ def test_decode_from_received_frames(gpu_ctx):
     out.free()
 
 
+@pytest.mark.parametrize("failed,batch", [([1, 4, 11, 13], 2), ([10, 11, 12, 13], 0), ([0, 1, 2, 3], 3),
+                                          ([5], 1), ([], 4)])
+def test_decode_frames_pipelined(gpu_ctx, failed, batch):
+    """nxec_decode_frames: the read path on received frames as one pipelined
+    call (gather of batch b + 1, decode of b, scatter of b - 1 at once) --
+    every stripe's k data chunks land in their output frames, equal to the
+    original data (oracle-encoded parity); frames of erased chunks are never
+    read (NULL entries); batches of 1-4 stripes, a ragged last batch, and the
+    default batch size."""
+    n, k, cs, ns = 14, 10, 65536 + 11, 9
+    enc = nxec.gen_rs_matrix(n, k)
+    data = [fill_bytes(k * cs, 8300 + s + 17 * len(failed)).reshape(k, cs) for s in range(ns)]
+    chunks = [np.concatenate([d, np.stack(oracle.matmul(enc[k:], list(d)))]) for d in data]
+    # every frame its own (pageable, odd-length) message buffer
+    msgs = [[np.frombuffer(bytes(chunks[s][c]), dtype=np.uint8).copy() for c in range(n)] for s in range(ns)]
+    in_frames = [0 if c in failed else msgs[s][c].ctypes.data for s in range(ns) for c in range(n)]
+    outs = [np.full(cs + 3, 0xEE, dtype=np.uint8) for _ in range(ns * k)]
+    gpu_ctx.decode_frames(n, k, failed, in_frames, [o.ctypes.data for o in outs], cs, ns, batch)
+    for s in range(ns):
+        for j in range(k):
+            assert np.array_equal(outs[s * k + j][:cs], data[s][j]), (s, j)
+            assert (outs[s * k + j][cs:] == 0xEE).all()
+    with pytest.raises(nxec.NxecError):  # a chosen input frame missing
+        bad = list(in_frames)
+        bad[next(c for c in range(n) if c not in failed)] = 0
+        gpu_ctx.decode_frames(n, k, failed, bad, [o.ctypes.data for o in outs], cs, ns, batch)
+
+
 @pytest.mark.parametrize("mode", ["pinned", "registered", "pageable"])
 def test_rs_recover_frames(gpu_ctx, mode):
     """Recover the failed chunks straight into their host frames: zero copy for
@@ -1436,6 +1464,11 @@ def test_encode_objects_async_pipeline(gpu_ctx, fused):
     want, _ = outputs(nxec.OBJECTS_TAIL_INPLACE)
     got, (ms, launches) = outputs(nxec.OBJECTS_TAIL_INPLACE | nxec.OBJECTS_ASYNC, timing=True)
     assert launches == len(batches) and ms > 0
+    # the whole-tail-arena form (the kernel stores every last-stripe data chunk) asynchronously too
+    want_all, _ = outputs(0)
+    got_all, _ = outputs(nxec.OBJECTS_ASYNC)
+    for w, g in zip(want_all, got_all):
+        assert all(np.array_equal(a, b) for a, b in zip(w, g))
     for (lengths, _, total, _, _), w, g in zip(batches, want, got):
         assert np.array_equal(w[2], g[2])  # digests
         pw, pg = w[0].reshape(total, p, M), g[0].reshape(total, p, M)
@@ -1600,18 +1633,21 @@ def test_encode_objects_last_stripe_at_a_page_end(gpu_ctx, flags):
     fl = nxec.OBJECTS_TAIL_INPLACE if flags == "inplace" else 0
     n, k, M = 14, 10, 4096
     p = n - k
-    picks = []  # (length, gap to the page end)
-    for L in range(200, 9 * M):
+    def falls_back(L, gap):  # the host's rule (nxec_objects.cpp): a whole chunk would read past the page
         cl = -(-L // k)
         cls = (cl + 15) // 16 * 16
-        jf, last = L // cl, L % cl
+        jf, pend = min(L // cl, k), L + gap
+        jov = (pend - cls) // cl + 1 if pend >= cls else 0
+        return jov < jf
+
+    picks = []  # (length, gap to the page end): fallbacks, then ordinary masked / whole ones
+    for L in range(16, 9 * M):
         for gap in (1, 7, 15):
-            if 0 < jf < k and cls - cl > last + gap:
-                picks.append((L, gap))
-        if len(picks) >= 24:
-            break
-    picks += [(L, 3) for L in (1000, 4095, 9999, 12345)]
-    assert len(picks) >= 24
+            if falls_back(L, gap) and sum(1 for _, _, f in picks if f) < 16:
+                picks.append((L, gap, True))
+    picks += [(L, 3, falls_back(L, 3)) for L in (1000, 4095, 9999, 12345, 10 * 1001, 10 * 77)]
+    assert sum(1 for _, _, f in picks if f) >= 8 and sum(1 for _, _, f in picks if not f) >= 3, picks
+    picks = [(L, gap) for L, gap, _ in picks]
     page = 4096
     npages = [(L + 16) // page + 1 for L, _ in picks]
     arena = nxec.DeviceBuffer(page * (sum(npages) + 2))

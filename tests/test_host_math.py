@@ -144,3 +144,18 @@ def test_survey_named_boundary(golden):
         assert out.tobytes().hex() == t["inv_hex"] and np.array_equal(src, before)
     z = np.zeros(9, dtype=np.uint8)
     assert lib.nxec_invert_matrix(z.ctypes.data, np.zeros(9, dtype=np.uint8).ctypes.data, 3) == -1
+
+
+def test_every_tool_is_cited():
+    """tools/ holds only what DESIGN.md, README.md, INTEGRATION.md, the
+    Makefile or a test cites (one-off scripts live in tools/archive, outside
+    the GPU push); at most 25 entries."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    entries = sorted(e for e in os.listdir(os.path.join(root, "tools")) if e not in ("archive", "__pycache__"))
+    assert len(entries) <= 25, entries
+    text = "".join(open(os.path.join(root, f)).read() for f in ("DESIGN.md", "README.md", "INTEGRATION.md", "Makefile"))
+    tdir = os.path.join(root, "tests")
+    text += "".join(open(os.path.join(tdir, f)).read() for f in os.listdir(tdir) if f.endswith(".py"))
+    missing = [e for e in entries if f"tools/{e}" not in text]
+    assert not missing, missing

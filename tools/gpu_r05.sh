@@ -102,4 +102,22 @@ if has sweep5b; then
     20,16,64 14,10,64 > $OUT/config5_layout_ab_b.log 2>&1 || { tail -5 $OUT/config5_layout_ab_b.log; stop sweep5b $?; }
   tail -3 $OUT/config5_layout_ab_b.log
 fi
+if has filesab; then
+  # same-box A/B of the multi-file write: product (fold, mask depth 3), the
+  # probe build with the fold off (round 4: pad copy + plain kernel), the
+  # probe build with the fold on (control), mask depth 4; alternating, twice
+  for r in 1 2; do
+    for v in prod nofold probes d4; do
+      case $v in
+        prod) lib=""; env="";;
+        nofold) lib=build/ab/probes/libnxec.so; env="NXEC_FILES_FOLD=0";;
+        probes) lib=build/ab/probes/libnxec.so; env="";;
+        d4) lib=build/ab/d4/libnxec.so; env="";;
+      esac
+      env $env ${lib:+NXEC_LIB=$ROOT/$lib} timeout -k 10 300 python bench.py --workload files --steps 30 --no-cpu-baseline \
+        --no-host-inclusive > $OUT/filesab_line.json 2>> $OUT/filesab.err || { tail -20 $OUT/filesab.err; stop "filesab $v" $?; }
+      python3 -c "import json; d=json.load(open('$OUT/filesab_line.json')); print('$v', d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['verified'], d['roofline']['lib_sha16'])" | tee -a $OUT/filesab.log
+    done
+  done
+fi
 echo "DONE $STEPS"
