@@ -222,14 +222,15 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * above: how DRAM channels and banks serve the k + rows streams of a column
  * depends on the chunk and stripe strides in ways no static rule captures
  * for every geometry (a 4 KiB chunk pad is worth +0.02 of 8
- * TB/s for RS(16,4) 256 KiB chunks and costs -0.11 at 1 MiB).  Times RS(n,k)
- * encode -- and, with NXEC_LAYOUT_RECOVER_HEAVY, a scattered n-k erasure
- * recover -- over a scratch batch of about budget_bytes (<= 0: 24 GiB, capped
- * at a quarter of the free device memory) for a few candidate layouts (the
- * table's, packed, chunk pads of 2, 4 and 8 KiB, an odd stripe stride) and
- * returns the fastest.  The result is cached per (device, n, k, len, flags);
- * the first call for a shape takes ~0.1-0.3 s.  Uses ctx's stream and
- * device; the scratch batch is freed before it returns. */
+ * TB/s for RS(16,4) 256 KiB chunks and costs -0.11 at 1 MiB).  Scores
+ * RS(n,k) encode, a contiguous and a scattered min(n-k,4)-erasure recover
+ * (equal weights; NXEC_LAYOUT_RECOVER_HEAVY doubles the scattered one) over a
+ * scratch batch of about budget_bytes (<= 0: 24 GiB, capped at a quarter of
+ * the free device memory) for a few candidate layouts (the table's, packed,
+ * chunk pads of 2, 4 and 8 KiB, an odd stripe stride); the table's layout
+ * stays unless another scores 1 % higher.  The result is cached per (device,
+ * n, k, len, flags); the first call for a shape takes ~0.3-1 s.  Uses ctx's
+ * stream and device; the scratch batch is freed before it returns. */
 int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
                             int64_t *chunk_stride, int64_t *stripe_stride);
 int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride);

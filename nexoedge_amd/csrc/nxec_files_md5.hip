@@ -22,14 +22,14 @@ namespace {
 
 // k_files_md5 reads HBM (a step of ~2 us is many load latencies): up to 4
 // steps in flight as k_mul_md5, as the 64-bit source pointers leave room (4
-// through k = 11, 3 through 14, then 2); the masked-chunk state takes one step
-// (3 and 4 steps measured the same in round 4), two from k = 13 (no spills)
+// through k = 11, 3 through 14, then 2); the masked-chunk state costs one
+// step from k = 11 and two from k = 13 (the deepest ring without spills)
 #ifndef NXEC_FM_MASK_DEPTH
-#define NXEC_FM_MASK_DEPTH 3  // design A/B: separate builds with -DNXEC_FM_MASK_DEPTH
+#define NXEC_FM_MASK_DEPTH 0  // design A/B: separate builds with -DNXEC_FM_MASK_DEPTH=D (0: by k)
 #endif
 template <int K, bool MASK>
 constexpr int fm_depth() {
-  constexpr int cap = !MASK ? 4 : K >= 13 ? 2 : NXEC_FM_MASK_DEPTH;
+  constexpr int cap = !MASK ? 4 : NXEC_FM_MASK_DEPTH ? NXEC_FM_MASK_DEPTH : K <= 10 ? 4 : K <= 12 ? 3 : 2;
   return gm_depth<K>() > cap ? cap : gm_depth<K>();
 }
 
@@ -137,9 +137,9 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     int64_t len0 = len_of(0);
     int lT = steps_of(len0), ltcl = max(tmax_of(len0), 0);
     const uint8_t *sp[K];
-    // MASK: the load cursor's masked chunk (K: none) and its bytes in the object
-    int lj = K;
-    int32_t lvm = 0;
+    // MASK: the load cursor's masked chunk (K: none) and the step at which
+    // this lane's vector of it reaches the object's end (-1: none)
+    int lj = K, lev = -1;
     // source pointers of the lane's column: a request's chunks, or -- a lane
     // whose column holds no byte of the request (chunks under 256 bytes) --
     // the scratch line: nothing past a chunk's 16-byte padding is read
@@ -149,7 +149,12 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         sp[j] = act && has ? reinterpret_cast<const uint8_t *>(q[li * rec + j]) + v * 16 : a.scratch + v * 16;
       if (MASK) {
         lj = act && has ? static_cast<int>(q[li * rec + K + a.p + 4] & 0xff) : K;
-        lvm = static_cast<int32_t>(q[li * rec + K + a.p + 3] >> 32);
+        lev = -1;
+        if (lj < K) {  // the first step whose load would reach past the object's last byte
+          const int32_t u = static_cast<int32_t>(q[li * rec + K + a.p + 3] >> 32) - v * 16 - 16;
+          const int e = u < 0 ? 0 : u / kEncMd5Step + 1;
+          lev = e <= ltcl ? e : -1;  // past ltcl the lane re-reads its last (in-object) vector
+        }
       }
     };
     set_src(0, tmax_of(len0) >= 0);
@@ -160,13 +165,12 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
         // step on the chunk reads the zero line (the vector across the end
         // gets its bytes from the compute step).  A rare, wave-uniform branch:
         // the step's loads below stay the plain kernel's.
-        const bool ev = lj < K && static_cast<int32_t>(off) + v * 16 + 16 > lvm;
+        const bool ev = lt == lev;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(ev) != 0, 0)) {
           if (ev) {
 #pragma unroll
             for (int j = 0; j < K; j++)
               if (j == lj) sp[j] = a.zero + v * 16;
-            lj = K;
           }
         }
       }
@@ -217,8 +221,9 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
     uint8_t *std_ = nullptr;
     int64_t scls = 0;
     int32_t sj0 = 0, sjm = -1, scl = 0;
-    // MASK: the compute request's masked chunk (K: none) and its bytes in the object
-    int cj = K;
+    // MASK: the compute request's masked chunk (K: none), its bytes in the
+    // object and the step whose vector of this lane straddles its end (-1: none)
+    int cj = K, chit = -1;
     int32_t cvm = 0;
     auto set_store = [&](int li) {
       if (!TSTORE && !MASK) return;
@@ -230,6 +235,10 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       cj = act ? static_cast<int>(m & 0xff) : K;
       sjm = (m >> 16) & 1 ? static_cast<int32_t>(m & 0xff) : -1;
       scl = static_cast<int32_t>(len_of(li));
+      if (MASK) {
+        const int32_t u = cvm - v * 16, r = u % kEncMd5Step;
+        chit = cj < K && u > 0 && r > 0 && r < 16 ? u / kEncMd5Step : -1;
+      }
     };
     set_store(0);
     auto run = [&](int step, u32x4(&d)[K]) {
@@ -243,7 +252,7 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       // object's last byte -- zero padded (the reference's padding,
       // chunk_manager.cc:390-399)
       if (MASK) {
-        const bool hit = ok && cj < K && pos < cvm && pos + 16 > cvm;
+        const bool hit = ok && ct == chit;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(hit) != 0, 0)) {
           u32x4 sv = u32x4{0u, 0u, 0u, 0u};
           if (hit) {

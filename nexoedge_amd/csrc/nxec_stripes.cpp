@@ -411,8 +411,9 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
   std::vector<std::pair<int64_t, int64_t>> cand = {{c0, s0}, {packed, n * packed}};
   for (int64_t pad : {int64_t(2048), int64_t(4096), int64_t(8192)}) cand.emplace_back(packed + pad, n * (packed + pad));
   cand.emplace_back(packed, (n + 1) * packed);  // an odd stripe stride in chunks
-  std::sort(cand.begin(), cand.end());
-  cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+  std::sort(cand.begin() + 1, cand.end());
+  cand.erase(std::unique(cand.begin() + 1, cand.end()), cand.end());
+  cand.erase(std::remove(cand.begin() + 1, cand.end(), cand[0]), cand.end());
   size_t free_b = 0, total_b = 0;
   NXEC_HIP(hipMemGetInfo(&free_b, &total_b));
   int64_t budget = budget_bytes > 0 ? budget_bytes : int64_t(24) << 30;
@@ -427,9 +428,11 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
   rc = hip_check(hipEventCreate(&e0), "hipEventCreate");
   if (!rc) rc = hip_check(hipEventCreate(&e1), "hipEventCreate");
   if (!rc) rc = launch_fill(d, static_cast<size_t>(budget), 0x7A11ull, st);
-  // a scattered recover (the slow patterns of DESIGN.md §3): the first
+  // the recovers scored beside the encode: the first min(n - k, 4) chunks,
+  // and a scattered set (the slow patterns of DESIGN.md §3): the first
   // min(n - k, 4) of chunks 1, 4, n - 3, n - 1 (the bench's {1,4,11,13} for RS(10,4))
-  std::vector<int32_t> scattered;
+  std::vector<int32_t> first, scattered;
+  for (int32_t c = 0; c < std::min(n - k, 4); c++) first.push_back(c);
   for (int32_t c : {1, 4, n - 3, n - 1})
     if (static_cast<int>(scattered.size()) < std::min(n - k, 4) && c >= 0 && c < n &&
         std::find(scattered.begin(), scattered.end(), c) == scattered.end())
@@ -441,30 +444,32 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
     if (rc) break;
     const int64_t ns = budget / c.second;
     if (ns < 1) continue;
-    auto timed = [&](bool recover, double *ms) {
+    // bytes per ms of one op (encode: (k + p) * len per stripe; recover: (k + e) * len)
+    auto rate_of = [&](const std::vector<int32_t> *erased, double *out) {
       auto op = [&]() {
-        return recover ? nxec_rs_recover_stripes(ctx, n, k, scattered.data(), static_cast<int>(scattered.size()), d,
-                                                 c.first, c.second, len, ns, st)
-                       : nxec_rs_encode_stripes(ctx, n, k, d, c.first, c.second, len, ns, st);
+        return erased ? nxec_rs_recover_stripes(ctx, n, k, erased->data(), static_cast<int>(erased->size()), d, c.first,
+                                                c.second, len, ns, st)
+                      : nxec_rs_encode_stripes(ctx, n, k, d, c.first, c.second, len, ns, st);
       };
       int r = op();  // warm
       if (!r) r = hip_check(hipEventRecord(e0, st), "hipEventRecord");
-      for (int i = 0; i < 3 && !r; i++) r = op();
+      for (int i = 0; i < 4 && !r; i++) r = op();
       if (!r) r = hip_check(hipEventRecord(e1, st), "hipEventRecord");
       float t = 0;
       if (!r) r = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
       if (!r) r = hip_check(hipEventElapsedTime(&t, e0, e1), "hipEventElapsedTime");
-      *ms = t / 3;
+      *out = double(ns) * (k + (erased ? double(erased->size()) : double(n - k))) * len / (t / 4);
       return r;
     };
-    double ms_enc = 0, ms_rec = 0;
-    if ((rc = timed(false, &ms_enc))) break;
-    double rate = double(ns) * n * len / ms_enc;  // encode bytes: (k + p) * len per stripe
-    if (flags & NXEC_LAYOUT_RECOVER_HEAVY) {
-      if ((rc = timed(true, &ms_rec))) break;
-      rate = 0.5 * rate + 0.5 * double(ns) * (k + double(scattered.size())) * len / ms_rec;
-    }
-    if (rate > best * 1.002) {  // ties keep the earlier (smaller-stride) candidate
+    // the score: encode, a contiguous and a scattered recover, equally weighted
+    // (RECOVER_HEAVY: the scattered one twice)
+    double r_enc = 0, r_first = 0, r_scat = 0;
+    if ((rc = rate_of(nullptr, &r_enc)) || (rc = rate_of(&first, &r_first)) || (rc = rate_of(&scattered, &r_scat)))
+      break;
+    const double w = (flags & NXEC_LAYOUT_RECOVER_HEAVY) ? 2.0 : 1.0;
+    const double rate = (r_enc + r_first + w * r_scat) / (2.0 + w);
+    // the table's layout (the first candidate) stays unless another beats it by 1 %
+    if (best < 0 || rate > best * 1.01) {
       best = rate;
       pick = c;
     }

@@ -103,21 +103,34 @@ if has sweep5b; then
   tail -3 $OUT/config5_layout_ab_b.log
 fi
 if has filesab; then
-  # same-box A/B of the multi-file write: product (fold, mask depth 3), the
+  # same-box A/B of the multi-file write: product (fold, mask ring by k), the
   # probe build with the fold off (round 4: pad copy + plain kernel), the
-  # probe build with the fold on (control), mask depth 4; alternating, twice
+  # probe build with the fold on (control), a 3-step mask ring; alternating, twice
   for r in 1 2; do
-    for v in prod nofold probes d4; do
+    for v in prod nofold probes d3; do
       case $v in
         prod) lib=""; env="";;
         nofold) lib=build/ab/probes/libnxec.so; env="NXEC_FILES_FOLD=0";;
         probes) lib=build/ab/probes/libnxec.so; env="";;
-        d4) lib=build/ab/d4/libnxec.so; env="";;
+        d3) lib=build/ab/d3/libnxec.so; env="";;
       esac
       env $env ${lib:+NXEC_LIB=$ROOT/$lib} timeout -k 10 300 python bench.py --workload files --steps 30 --no-cpu-baseline \
         --no-host-inclusive > $OUT/filesab_line.json 2>> $OUT/filesab.err || { tail -20 $OUT/filesab.err; stop "filesab $v" $?; }
       python3 -c "import json; d=json.load(open('$OUT/filesab_line.json')); print('$v', d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['verified'], d['roofline']['lib_sha16'])" | tee -a $OUT/filesab.log
     done
   done
+fi
+if has filesalign; then
+  # the fold's cost split: aligned in-place reads vs masked chunks vs raw sizes
+  for v in prod nofold; do
+    case $v in
+      prod) lib=""; env="";;
+      nofold) lib=build/ab/probes/libnxec.so; env="NXEC_FILES_FOLD=0";;
+    esac
+    echo "== $v" >> $OUT/files_align.log
+    env $env ${lib:+NXEC_LIB=$ROOT/$lib} timeout -k 10 300 python3 -u tools/files_align_probe.py >> $OUT/files_align.log 2>&1 \
+      || { tail -20 $OUT/files_align.log; stop "filesalign $v" $?; }
+  done
+  cat $OUT/files_align.log
 fi
 echo "DONE $STEPS"
