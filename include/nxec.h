@@ -518,7 +518,7 @@ int nxec_rs_recover_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * alignment, pageable or pinned); only the k chunks rs.cc:252-265 chooses are
  * read (entries of failed chunks may be NULL).  All k data chunks of stripe s
  * are written to out_frames[s*k + j].  The stripes go through HBM in batches
- * of batch_stripes (<= 0: about 64 MiB of chunks per batch) on three streams:
+ * of batch_stripes (<= 0: about 128 MiB of chunks per batch) on three streams:
  * the gather of batch b + 1 (host -> device), the decode of batch b and the
  * scatter of batch b - 1 (device -> host) run at once, so both PCIe
  * directions and the host copy pool are busy together.  Synchronous. */

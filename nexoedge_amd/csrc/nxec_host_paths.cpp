@@ -429,7 +429,7 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
       (rc = nxec_rs_decode_matrix(n, k, inputs.data(), targets.data(), static_cast<int>(targets.size()), dm.data())))
     return rc;
   const int64_t stride = (len + 15) / 16 * 16;
-  int64_t B = batch_stripes > 0 ? batch_stripes : std::max<int64_t>(1, (int64_t(64) << 20) / (int64_t(k) * stride));
+  int64_t B = batch_stripes > 0 ? batch_stripes : std::max<int64_t>(1, (int64_t(128) << 20) / (int64_t(k) * stride));
   B = std::min(B, nstripes);
   const int64_t nb = (nstripes + B - 1) / B;
   std::unique_lock<std::mutex> lk;
@@ -472,29 +472,24 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
       }
     });
   };
+  // one gather / scatter call per batch: row (i, j) of a batch is chunk i * k + j at `stride`
   std::thread gatherer = run_stage([&]() {
-    std::vector<const unsigned char *> fr(static_cast<size_t>(B));
+    std::vector<const unsigned char *> fr(static_cast<size_t>(B * k));
     for (int64_t b = 0; b < nb; b++) {
       if (b >= kObjSlots && !wait_for(scattered, b - kObjSlots + 1)) return;  // the slot's previous batch has left
       const int64_t s0 = b * B, m = std::min(B, nstripes - s0);
-      for (int j = 0; j < k; j++) {
-        for (int64_t i = 0; i < m; i++) fr[size_t(i)] = in_frames[(s0 + i) * n + inputs[j]];
-        if (int r = nxec_gather_chunks(ctx, fr.data(), m, len, in_rows(b) + j * stride, int64_t(k) * stride, s_gather))
-          return fail(r);
-      }
+      for (int64_t i = 0; i < m; i++)
+        for (int j = 0; j < k; j++) fr[size_t(i * k + j)] = in_frames[(s0 + i) * n + inputs[j]];
+      if (int r = nxec_gather_chunks(ctx, fr.data(), m * k, len, in_rows(b), stride, s_gather)) return fail(r);
       done(gathered);
     }
   });
   std::thread scatterer = run_stage([&]() {
-    std::vector<unsigned char *> fr(static_cast<size_t>(B));
     for (int64_t b = 0; b < nb; b++) {
       if (!wait_for(decoded, b + 1)) return;
       const int64_t s0 = b * B, m = std::min(B, nstripes - s0);
-      for (int j = 0; j < k; j++) {
-        for (int64_t i = 0; i < m; i++) fr[size_t(i)] = out_frames[(s0 + i) * k + j];
-        if (int r = nxec_scatter_chunks(ctx, out_rows(b) + j * stride, int64_t(k) * stride, m, len, fr.data(), s_scatter))
-          return fail(r);
-      }
+      if (int r = nxec_scatter_chunks(ctx, out_rows(b), stride, m * k, len, out_frames + s0 * k, s_scatter))
+        return fail(r);
       done(scattered);
     }
   });

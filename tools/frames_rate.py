@@ -1,5 +1,7 @@
 """Chunk-frame gather / scatter rates (nxec_gather_chunks / nxec_scatter_chunks):
 pageable and pinned frames, 1 MiB chunks, alone and with concurrent callers.
+FRAMES_READ=1: the bench's read path (nxec_decode_frames vs the sequential
+calls) under the pool size NXEC_HOST_THREADS gives.
 Run on the GPU box: python tools/frames_rate.py"""
 import os
 import sys
@@ -121,6 +123,15 @@ if os.environ.get("FRAMES_ASYNC"):  # only the one-caller duplex legs
         for a in (False, True, False, True):
             print(f"one caller gather+scatter pinned-in={pinned!s:5s} {'async' if a else 'sync '}: "
                   f"{one_caller_duplex(a, pinned):6.2f} GiB/s", flush=True)
+    sys.exit(0)
+
+if os.environ.get("FRAMES_READ"):  # the bench's read path (nxec_decode_frames) under this pool size
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench  # noqa: E402
+    bench.nxec = nxec
+    ctx = nxec.Context(0)
+    r = bench.read_from_frames(ctx, 14, 10, cs, 256)
+    print(f"read path NXEC_HOST_THREADS={os.environ.get('NXEC_HOST_THREADS', '8')}: {r}", flush=True)
     sys.exit(0)
 
 if os.environ.get("FRAMES_QUICK"):  # one pageable gather pass (for a profiler timeline)

@@ -1,10 +1,9 @@
+# one-off GPU call: read-path pool-size A/B, then the decode_frames tests
 set -o pipefail
 OUT=gpurun_out
-timeout -k 10 300 python bench.py --gpus 8 --group --stripes 512 --steps 10 --warmup 2 --no-cpu-baseline --no-host-inclusive > $OUT/group8.json 2> $OUT/group8.err || { tail -20 $OUT/group8.err; exit 1; }
-python3 -c "import json; d=json.load(open('$OUT/group8.json')); print('group8', d['value'], d['n_gpus'], d.get('verified'), json.dumps(d.get('group'))[:400])"
-for r in 1 2; do
-for lay in auto recover tuned; do
-  timeout -k 10 300 python bench.py --layout $lay --steps 30 --no-cpu-baseline --no-host-inclusive > $OUT/head_line.json 2>> $OUT/head.err || { tail -20 $OUT/head.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/head_line.json')); print('$lay', d['value'], d['roofline']['frac'], d['verified'], d['config']['layout'])" | tee -a $OUT/headab.log
+for t in 8 16 12 8 16; do
+  NXEC_HOST_THREADS=$t FRAMES_READ=1 timeout -k 10 240 python3 -u tools/frames_rate.py >> $OUT/frames_read.log 2>&1 || { tail -20 $OUT/frames_read.log; exit 1; }
 done
-done
+cat $OUT/frames_read.log
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "frames" > $OUT/pytest_frames.log 2>&1 || { tail -30 $OUT/pytest_frames.log; exit 1; }
+tail -2 $OUT/pytest_frames.log
