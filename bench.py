@@ -971,6 +971,10 @@ def main():
         }
         if kt:
             result["roofline"]["kernel_timing"] = kt
+        if world > nxec.device_count():
+            result["roofline"]["shared_device"] = (
+                f"{world} ranks on {nxec.device_count()} GPU(s), round-robin (a rehearsal of the multi-rank path): "
+                "each launch ran beside the other ranks' launches, so the per-launch rate is not the kernel's")
         if ceiling:
             result["roofline"]["on_box_ceiling"] = ceiling
         if wl.name == "rs10_4":

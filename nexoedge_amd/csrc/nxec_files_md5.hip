@@ -248,18 +248,32 @@ __global__ __launch_bounds__(kEmBlock) void k_files_md5(const FilesMd5Args a) {
       uint8_t *rb = row + (step & 1) * buf_bytes;
       const int32_t pos = ct * kEncMd5Step + v * 16;
       // MASK: this lane's vector of chunk cj straddles the object's end (it was
-      // loaded as zeros): read its valid bytes one by one -- nothing past the
-      // object's last byte -- zero padded (the reference's padding,
-      // chunk_manager.cc:390-399)
+      // loaded as zeros): its valid bytes from the 16-byte aligned blocks that
+      // hold them (an aligned block with a byte of the object never crosses a
+      // page past it), shifted into place, the rest zero (the reference's
+      // padding, chunk_manager.cc:390-399).  Two vector loads, not a load per
+      // byte: the wave waits for them once.
       if (MASK) {
         const bool hit = ok && ct == chit;
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(hit) != 0, 0)) {
           u32x4 sv = u32x4{0u, 0u, 0u, 0u};
           if (hit) {
-            const uint8_t *pb = reinterpret_cast<const uint8_t *>(q[cr * rec + cj]) + pos;
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            for (int b = 0; b < cvm - pos; b++) w[b >> 2] |= static_cast<uint32_t>(pb[b]) << (8 * (b & 3));
-            sv = u32x4{w[0], w[1], w[2], w[3]};
+            const uintptr_t at = static_cast<uintptr_t>(q[cr * rec + cj]) + pos;
+            const int nv = cvm - pos, r = static_cast<int>(at & 15), qd = r >> 2, sh = r & 3;
+            const uint8_t *blk = reinterpret_cast<const uint8_t *>(at - r);
+            const u32x4 lo = dev::ld_global(blk);
+            const u32x4 hi = r + nv > 16 ? dev::ld_global(blk + 16) : u32x4{0u, 0u, 0u, 0u};
+            const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+            uint32_t y[5], o[4];
+#pragma unroll
+            for (int m = 0; m < 5; m++) y[m] = qd == 0 ? w[m] : qd == 1 ? w[m + 1] : qd == 2 ? w[m + 2] : w[m + 3];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+              const int keep = nv - 4 * i;  // bytes of this word inside the object
+              const uint32_t mask = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+              o[i] = __builtin_amdgcn_alignbyte(y[i + 1], y[i], static_cast<uint32_t>(sh)) & mask;
+            }
+            sv = u32x4{o[0], o[1], o[2], o[3]};
           }
 #pragma unroll
           for (int j = 0; j < K; j++)

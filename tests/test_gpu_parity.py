@@ -1558,7 +1558,8 @@ def test_encode_objects_async_threads(gpu_ctx):
 
 
 @pytest.mark.parametrize("n,k,M,nfiles", [(14, 10, 4096, 700), (14, 10, 65536, 300), (6, 4, 1000 * 16, 200),
-                                          (20, 16, 2048, 5000)])
+                                          (20, 16, 2048, 5000), (12, 9, 8192, 400), (18, 14, 2048, 900),
+                                          (17, 15, 2048, 600)])
 def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
     """NXEC_OBJECTS_TAIL_INPLACE (include/nxec.h): parity and every digest equal
     the default call's; each last stripe's partial data chunk is in its tail
@@ -1566,7 +1567,8 @@ def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
     digests equal hashlib's of those bytes), all-zero ones are zeros (digest of
     cl zero bytes).  Other tail slots are unspecified: if one was written, it
     holds that chunk zero-padded (the one-launch path copies the chunks it
-    does not read in place there first)."""
+    does not read in place there first).  k = 9-16: the masked kernel's
+    register ring at every depth it takes (4 through k = 10, 3, then 2)."""
     import hashlib
     p = n - k
     rng = np.random.default_rng(3 * nfiles + k)

@@ -23,15 +23,18 @@ ctx = nxec.Context(0)
 raw = [int(x) for x in np.random.default_rng(1234).integers(1, 2 * k * M + 1, size=4096)]
 
 
-def aligned(L, minus):
+def aligned(L, minus, a=16):
     ns, nf, cl = nxec.object_layout(n, k, L, M)
     if ns == nf:
         return L
-    c16 = min((cl + 15) // 16 * 16, M)
-    return nf * k * M + k * c16 - minus
+    c = min((cl + a - 1) // a * a, M)
+    if a < 16 and c % 16 == 0 and c + a <= M:
+        c += a  # a-byte aligned, not 16
+    return nf * k * M + k * c - minus
 
 
-variants = {"raw": raw, "a16": [aligned(L, 0) for L in raw], "a16m": [aligned(L, 8) for L in raw]}
+variants = {"raw": raw, "a16": [aligned(L, 0) for L in raw], "a16m": [aligned(L, 8) for L in raw],
+            "a4m": [aligned(L, 8, 4) for L in raw], "a8m": [aligned(L, 8, 8) for L in raw]}
 for name, lengths in variants.items():
     offs = np.concatenate([[0], np.cumsum([(L + 15) // 16 * 16 for L in lengths])])
     arena = nxec.DeviceBuffer(int(offs[-1]))

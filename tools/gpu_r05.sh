@@ -103,16 +103,14 @@ if has sweep5b; then
   tail -3 $OUT/config5_layout_ab_b.log
 fi
 if has filesab; then
-  # same-box A/B of the multi-file write: product (fold, mask ring by k), the
-  # probe build with the fold off (round 4: pad copy + plain kernel), the
-  # probe build with the fold on (control), a 3-step mask ring; alternating, twice
+  # same-box A/B of the multi-file write: product (the fold), the probe build
+  # with the fold off (round 4: pad copy + plain kernel); alternating, twice
   for r in 1 2; do
-    for v in prod nofold probes d3; do
+    for v in prod nofold; do
       case $v in
         prod) lib=""; env="";;
         nofold) lib=build/ab/probes/libnxec.so; env="NXEC_FILES_FOLD=0";;
         probes) lib=build/ab/probes/libnxec.so; env="";;
-        d3) lib=build/ab/d3/libnxec.so; env="";;
       esac
       env $env ${lib:+NXEC_LIB=$ROOT/$lib} timeout -k 10 300 python bench.py --workload files --steps 30 --no-cpu-baseline \
         --no-host-inclusive > $OUT/filesab_line.json 2>> $OUT/filesab.err || { tail -20 $OUT/filesab.err; stop "filesab $v" $?; }

@@ -16,7 +16,7 @@ def rows(d, sub):
     path = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0]
     out = {}
     for r in csv.DictReader(open(path)):
-        if sub in r["Kernel_Name"]:
+        if sub.replace(" ", "") in r["Kernel_Name"].replace(" ", ""):  # spacing of template arguments varies
             out[int(r["Dispatch_Id"])] = (float(r["Counter_Value"]), r["Kernel_Name"])
     return out
 
