@@ -211,15 +211,17 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    # round-4 passes on the shipped library (tools/archive/gpu_r04_final.sh; every dispatch
+    # round-5 passes on the shipped library (tools/gpu_r05_final.sh; every dispatch
     # of the roofline kernel labelled with the bench line's bytes per launch);
-    # tests/test_bench_line.py checks each file's lib_sha16 against libnxec.so;
-    # only the default layout the passes ran with (other layouts report traffic null)
-    ("rs10_4", 1 << 20, "auto"): ("r04_pmc_rs10_4.json", "encode_recover"),
-    ("mixed16", 4 << 20, "auto"): ("r04_pmc_mixed16.json", "encode_recover"),
-    ("write14", 1 << 20, "auto"): ("r04_pmc_write14.json", "encode_md5_fused"),
-    ("repair12", 1 << 20, "auto"): ("r04_pmc_repair12.json", "repair_fused_perm12"),
-    ("files", 1 << 20, "auto"): ("r04_pmc_files.json", "encode_objects_md5"),
+    # tests/test_bench_line.py checks each file's labels and reports its lib_sha16
+    # against libnxec.so; only the default layout the passes ran with (other
+    # layouts report traffic null)
+    ("rs10_4", 1 << 20, "auto"): ("r05_pmc_rs10_4.json", "encode_recover"),
+    ("decode_full", 1 << 20, "auto"): ("r05_pmc_decode_full.json", "decode_full"),
+    ("mixed16", 4 << 20, "auto"): ("r05_pmc_mixed16.json", "encode_recover"),
+    ("write14", 1 << 20, "auto"): ("r05_pmc_write14.json", "encode_md5_fused"),
+    ("repair12", 1 << 20, "auto"): ("r05_pmc_repair12.json", "repair_fused_perm12"),
+    ("files", 1 << 20, "auto"): ("r05_pmc_files.json", "encode_objects_md5"),
 }
 
 
@@ -566,9 +568,9 @@ def wl_files(args, ctx, stream, rank):
                        if ns > nf and (L - nf * k * M) % cl)
     # k_files_md5's own bytes per launch: every request's k data chunks read
     # (last stripes: in place from the object, the chunks past the data from
-    # the zero line) and p parity chunks written, at the request's chunk length;
-    # the kernel also writes each partial chunk to its tail slot (tail_written)
-    kernel_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts)
+    # the zero line) and p parity chunks written, at the request's chunk
+    # length, plus each partial chunk's zero-padded tail-slot store (tail_written)
+    kernel_bytes = sum((nf * M + (ns - nf) * cl) * n for ns, nf, cl in layouts) + tail_written
     longest, nreq = files_longest_slot(n, k, M, lengths)
     # NXEC_OBJECTS_ASYNC: the host plans batch i + 1 while batch i codes (the
     # timed region ends with a stream sync)
@@ -584,7 +586,8 @@ def wl_files(args, ctx, stream, rank):
               "byte_accounting": "value: HBM side of the call, the write14 convention: data read + parity "
                                  f"written + tail-arena writes ({user / 2**30:.1f} + {parity_bytes / 2**30:.1f} + "
                                  f"{tail_written / 2**30:.1f} GiB), the MD5 of every chunk reads LDS; roofline: "
-                                 f"k_files_md5 alone, (k + p) x chunk length per request ({kernel_bytes / 2**30:.2f} "
+                                 f"k_files_md5 alone, (k + p) x chunk length per request + the partial chunks' tail-slot "
+                                 f"stores ({kernel_bytes / 2**30:.2f} "
                                  "GiB), timed by HIP events around its launch inside the library",
               "host": "nxec_encode_objects_ex(NXEC_OBJECTS_ASYNC): the host plan of step i + 1 overlaps step i",
               "md5_chain_floor": {"longest_slot_steps": longest, "us_per_step": round(MD5_STEP_US, 3),

@@ -74,7 +74,7 @@ def test_pmc_summaries_are_labelled_passes():
 
     h = bench.lib_sha16()
     files = {v[0]: v[1] for v in bench.PMC_SUMMARIES.values()}
-    assert {w for w, _, _ in bench.PMC_SUMMARIES} >= {"rs10_4", "write14", "repair12", "files", "mixed16"}
+    assert {w for w, _, _ in bench.PMC_SUMMARIES} >= {"rs10_4", "decode_full", "write14", "repair12", "files", "mixed16"}
     for name, op in files.items():
         with open(os.path.join(ROOT, "profiles", name)) as f:
             doc = json.load(f)
