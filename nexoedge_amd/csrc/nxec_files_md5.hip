@@ -23,7 +23,8 @@ namespace {
 // k_files_md5 reads HBM (a step of ~2 us is many load latencies): up to 4
 // steps in flight as k_mul_md5, as the 64-bit source pointers leave room (4
 // through k = 11, 3 through 14, then 2); the masked-chunk state costs one
-// step from k = 11 and two from k = 13 (the deepest ring without spills)
+// step from k = 11 and two from k = 13 (the deepest ring without spills;
+// 3 and 4 steps measured the same at k = 10, profiles/r05_files_fold_ab.log)
 #ifndef NXEC_FM_MASK_DEPTH
 #define NXEC_FM_MASK_DEPTH 0  // design A/B: separate builds with -DNXEC_FM_MASK_DEPTH=D (0: by k)
 #endif
@@ -61,11 +62,14 @@ constexpr int fm_depth() {
 // past the data at an all-zero line.  MASK: a request may name one data
 // chunk jm that holds the object's last bytes (vm of them, fewer than the
 // chunk length): the lane's vectors of that chunk are read in place while
-// they lie inside the data, the one vector that straddles the end is read
-// byte by byte (nothing past the object's last byte is touched) and zero
-// padded, and from there on the chunk reads the zero line -- no pad copy
-// before the launch.  Both are rare per-lane events (one wave-uniform test
-// per step), so the step loop keeps the tail-free form.  With store mode 1
+// they lie inside the data, the one vector that straddles the end is rebuilt
+// from the aligned 16-byte blocks holding its bytes (never a page past the
+// object's last byte) and zero padded, and from there on the chunk reads the
+// zero line -- no pad copy before the launch.  Both are rare per-lane events
+// at steps computed once per request (one wave-uniform test per step), so the
+// step loop keeps the tail-free form.  Chunks that start off a 4-byte
+// boundary (a last stripe's chunk j at j * cl) are loaded as they lie: the
+// shifted-load alternatives lost.  With store mode 1
 // the code lanes also write that chunk, zero padded, to its tail-arena slot
 // (NXEC_OBJECTS_TAIL_INPLACE: the one chunk of a last stripe the caller
 // sends from the arena).  TSTORE (whole tail arena, no flag): the code lanes

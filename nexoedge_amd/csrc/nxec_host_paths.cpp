@@ -473,7 +473,9 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
     });
   };
   // one gather / scatter call per batch: row (i, j) of a batch is chunk i * k + j at `stride`
-  std::thread gatherer = run_stage([&]() {
+  std::thread gatherer, scatterer;
+  try {  // a stage that cannot start fails the call; the other one sees the error and stops
+  gatherer = run_stage([&]() {
     std::vector<const unsigned char *> fr(static_cast<size_t>(B * k));
     for (int64_t b = 0; b < nb; b++) {
       if (b >= kObjSlots && !wait_for(scattered, b - kObjSlots + 1)) return;  // the slot's previous batch has left
@@ -484,7 +486,7 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
       done(gathered);
     }
   });
-  std::thread scatterer = run_stage([&]() {
+  scatterer = run_stage([&]() {
     for (int64_t b = 0; b < nb; b++) {
       if (!wait_for(decoded, b + 1)) return;
       const int64_t s0 = b * B, m = std::min(B, nstripes - s0);
@@ -493,6 +495,9 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
       done(scattered);
     }
   });
+  } catch (const std::exception &e) {
+    fail(set_error(NXEC_ERR_NOMEM, "nxec_decode_frames: %s", e.what()));
+  }
   for (int64_t b = 0; b < nb; b++) {  // decode on the calling thread
     if (!wait_for(gathered, b + 1)) break;
     const int64_t m = std::min(B, nstripes - b * B);
@@ -506,8 +511,8 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
     }
     done(decoded);
   }
-  gatherer.join();
-  scatterer.join();
+  if (gatherer.joinable()) gatherer.join();
+  if (scatterer.joinable()) scatterer.join();
   for (int i = 0; i < kObjSlots; i++) (void)hipStreamSynchronize(stg.streams[i]);
   if (!lk.owns_lock()) priv.release();
   if (err) restore_error(err_msg);

@@ -270,7 +270,7 @@ struct FilesMd5Args {
   //                 the masked chunk that lie in the object
   //   last_mask[s]  jm | j0 << 8 | mode << 16: the masked data chunk (k:
   //                 none) -- read in place below vm, zero padded from vm, the
-  //                 vector across vm read byte by byte --, the chunks a
+  //                 vector across vm rebuilt from aligned blocks --, the chunks a
   //                 whole-tail-arena call stores (j < j0), mode 1: store the
   //                 masked chunk zero padded to its slot
   const uint64_t *last_slot;
