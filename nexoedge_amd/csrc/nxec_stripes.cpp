@@ -438,40 +438,47 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
         std::find(scattered.begin(), scattered.end(), c) == scattered.end())
       scattered.push_back(c);
   std::sort(scattered.begin(), scattered.end());
+  // every candidate scored in two interleaved rounds (the device's state
+  // drifts less between candidates than between calls), scores summed
+  std::vector<double> score(cand.size(), 0.0);
+  for (int round = 0; round < 2 && !rc; round++) {
+    for (size_t ci = 0; ci < cand.size() && !rc; ci++) {
+      const auto &c = cand[ci];
+      const int64_t ns = budget / c.second;
+      if (ns < 1) continue;
+      // bytes per ms of one op (encode: (k + p) * len per stripe; recover: (k + e) * len)
+      auto rate_of = [&](const std::vector<int32_t> *erased, double *out) {
+        auto op = [&]() {
+          return erased ? nxec_rs_recover_stripes(ctx, n, k, erased->data(), static_cast<int>(erased->size()), d,
+                                                  c.first, c.second, len, ns, st)
+                        : nxec_rs_encode_stripes(ctx, n, k, d, c.first, c.second, len, ns, st);
+        };
+        int r = op();  // warm
+        if (!r) r = hip_check(hipEventRecord(e0, st), "hipEventRecord");
+        for (int i = 0; i < 4 && !r; i++) r = op();
+        if (!r) r = hip_check(hipEventRecord(e1, st), "hipEventRecord");
+        float t = 0;
+        if (!r) r = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
+        if (!r) r = hip_check(hipEventElapsedTime(&t, e0, e1), "hipEventElapsedTime");
+        *out = double(ns) * (k + (erased ? double(erased->size()) : double(n - k))) * len / (t / 4);
+        return r;
+      };
+      // the score: encode, a contiguous and a scattered recover, equally weighted
+      // (RECOVER_HEAVY: the scattered one twice)
+      double r_enc = 0, r_first = 0, r_scat = 0;
+      if ((rc = rate_of(nullptr, &r_enc)) || (rc = rate_of(&first, &r_first)) || (rc = rate_of(&scattered, &r_scat)))
+        break;
+      const double w = (flags & NXEC_LAYOUT_RECOVER_HEAVY) ? 2.0 : 1.0;
+      score[ci] += (r_enc + r_first + w * r_scat) / (2.0 + w);
+    }
+  }
+  // the table's layout (the first candidate) stays unless another scores 0.5 % higher
   double best = -1;
   std::pair<int64_t, int64_t> pick = {c0, s0};
-  for (const auto &c : cand) {
-    if (rc) break;
-    const int64_t ns = budget / c.second;
-    if (ns < 1) continue;
-    // bytes per ms of one op (encode: (k + p) * len per stripe; recover: (k + e) * len)
-    auto rate_of = [&](const std::vector<int32_t> *erased, double *out) {
-      auto op = [&]() {
-        return erased ? nxec_rs_recover_stripes(ctx, n, k, erased->data(), static_cast<int>(erased->size()), d, c.first,
-                                                c.second, len, ns, st)
-                      : nxec_rs_encode_stripes(ctx, n, k, d, c.first, c.second, len, ns, st);
-      };
-      int r = op();  // warm
-      if (!r) r = hip_check(hipEventRecord(e0, st), "hipEventRecord");
-      for (int i = 0; i < 4 && !r; i++) r = op();
-      if (!r) r = hip_check(hipEventRecord(e1, st), "hipEventRecord");
-      float t = 0;
-      if (!r) r = hip_check(hipEventSynchronize(e1), "hipEventSynchronize");
-      if (!r) r = hip_check(hipEventElapsedTime(&t, e0, e1), "hipEventElapsedTime");
-      *out = double(ns) * (k + (erased ? double(erased->size()) : double(n - k))) * len / (t / 4);
-      return r;
-    };
-    // the score: encode, a contiguous and a scattered recover, equally weighted
-    // (RECOVER_HEAVY: the scattered one twice)
-    double r_enc = 0, r_first = 0, r_scat = 0;
-    if ((rc = rate_of(nullptr, &r_enc)) || (rc = rate_of(&first, &r_first)) || (rc = rate_of(&scattered, &r_scat)))
-      break;
-    const double w = (flags & NXEC_LAYOUT_RECOVER_HEAVY) ? 2.0 : 1.0;
-    const double rate = (r_enc + r_first + w * r_scat) / (2.0 + w);
-    // the table's layout (the first candidate) stays unless another beats it by 1 %
-    if (best < 0 || rate > best * 1.01) {
-      best = rate;
-      pick = c;
+  for (size_t ci = 0; ci < cand.size(); ci++) {
+    if (score[ci] > 0 && (best < 0 || score[ci] > best * 1.005)) {
+      best = score[ci];
+      pick = cand[ci];
     }
   }
   if (e0) (void)hipEventDestroy(e0);
