@@ -264,6 +264,32 @@ def test_product_build_and_round4_entry_points_without_a_device():
                                                None) == _lib.NXEC_ERR_INVALID
 
 
+def test_round5_entry_points_without_a_device():
+    """The round-5 entry points validate before any device use: the layout
+    calibration and the pipelined frames read refuse a missing context or
+    bad geometry, and an empty read (no stripes, or zero-length chunks) is a
+    no-op (with no stripes, no frame tables are needed)."""
+    cs, ss = ctypes.c_int64(-1), ctypes.c_int64(-1)
+    L = _lib.lib
+    assert L.nxec_batch_layout_tuned(None, 14, 10, 1 << 20, 0, 0, ctypes.byref(cs), ctypes.byref(ss)) == \
+        _lib.NXEC_ERR_INVALID
+    assert (cs.value, ss.value) == (-1, -1)
+    f = (ctypes.c_int32 * 4)(6, 7, 8, 9)
+    fr = (ctypes.c_void_p * 14)()
+    out = (ctypes.c_void_p * 10)()
+    assert L.nxec_decode_frames(None, 14, 10, f, 4, fr, out, 1 << 20, 1, 0) == _lib.NXEC_ERR_INVALID
+    assert b"nxec_decode_frames" in L.nxec_last_error() or b"invalid" in L.nxec_last_error()
+    # bad geometry / negative sizes / missing frame tables are refused before the context is touched
+    fake = ctypes.c_void_p(1)  # never dereferenced: validation fails first
+    assert L.nxec_decode_frames(fake, 3, 4, f, 0, fr, out, 16, 1, 0) == _lib.NXEC_ERR_INVALID
+    assert L.nxec_decode_frames(fake, 14, 10, f, 4, fr, out, -1, 1, 0) == _lib.NXEC_ERR_INVALID
+    assert L.nxec_decode_frames(fake, 14, 10, f, 4, None, out, 16, 1, 0) == _lib.NXEC_ERR_INVALID
+    assert L.nxec_decode_frames(fake, 14, 10, None, 4, fr, out, 16, 1, 0) == _lib.NXEC_ERR_INVALID
+    # nothing to read: no frames needed, no device touched
+    assert L.nxec_decode_frames(fake, 14, 10, f, 4, None, None, 16, 0, 0) == _lib.NXEC_OK
+    assert L.nxec_decode_frames(fake, 14, 10, f, 4, fr, out, 0, 1, 0) == _lib.NXEC_OK
+
+
 DEPLOYMENT_SETTINGS = {"NXEC_HOST_THREADS", "NXEC_HOST_DIRECT", "NXEC_SLOT_POOL_MAX", "NXEC_HOST_ARENA_MAX",
                        "NXEC_CHUNK_ARENA_MIN", "NXEC_CHUNK_MD5", "NXEC_DIGEST_PLACE", "NXEC_DIGEST_THREADS",
                        "NXEC_DIGEST_CPUS"}
