@@ -548,6 +548,50 @@ def test_encode_decode_object(gpu_ctx, n, k, M, length):
         b.free()
 
 
+def test_batch_layout_tuned(gpu_ctx):
+    """nxec_batch_layout_tuned (include/nxec.h): the device-measured layout is
+    one of the documented candidates (the table's, packed, +2/4/8 KiB chunk
+    pads, an odd stripe stride), the same on a second call (cached per shape
+    and flags), and a batch laid out at those strides encodes and recovers
+    bit-exactly against the oracle; n == k is refused."""
+    n, k, cs, ns = 8, 6, 4096 + 48, 5
+    budget = 256 << 20
+    packed = rup(cs)
+    cands = {(packed, n * packed), (packed, (n + 1) * packed)}
+    cands |= {(packed + pad, n * (packed + pad)) for pad in (2048, 4096, 8192)}
+    for flags in (0, nxec.LAYOUT_RECOVER_HEAVY):
+        first = gpu_ctx.batch_layout_tuned(n, k, cs, flags, budget)
+        assert first in cands | {nxec.batch_layout(n, cs, flags)}, (flags, first)
+        assert gpu_ctx.batch_layout_tuned(n, k, cs, flags, budget) == first
+    cst, sst = gpu_ctx.batch_layout_tuned(n, k, cs, 0, budget)
+    data = [fill_bytes(k * cs, 9100 + s).reshape(k, cs) for s in range(ns)]
+    host = np.full((ns, sst), 0x5A, dtype=np.uint8)
+    for s in range(ns):
+        for j in range(k):
+            host[s, j * cst: j * cst + cs] = data[s][j]
+    b = up(host)
+    gpu_ctx.rs_encode(n, k, b.ptr, cst, sst, cs, ns)
+    gpu_ctx.sync()
+    enc = nxec.gen_rs_matrix(n, k)
+    full = b.download().reshape(ns, sst)
+    want = [oracle.matmul(enc[k:], list(data[s])) for s in range(ns)]
+    for s in range(ns):
+        for i in range(n - k):
+            assert np.array_equal(full[s, (k + i) * cst: (k + i) * cst + cs], want[s][i]), (s, i)
+    failed = [1, k]  # a data chunk and a parity chunk
+    lost = full.copy()
+    for s in range(ns):
+        for c in failed:
+            lost[s, c * cst: c * cst + cs] = 0
+    b.upload(lost.reshape(-1))
+    gpu_ctx.rs_recover(n, k, failed, b.ptr, cst, sst, cs, ns)
+    gpu_ctx.sync()
+    assert np.array_equal(b.download().reshape(ns, sst), full)
+    b.free()
+    with pytest.raises(nxec.NxecError):
+        gpu_ctx.batch_layout_tuned(n, n, cs)
+
+
 # ------------------------------------------------------------ agent service (§8f.3)
 @pytest.mark.parametrize("batch_bytes", [0, 3 * 8192])
 def test_agent_encode_batch(gpu_ctx, batch_bytes):
