@@ -1,12 +1,10 @@
-# one-off GPU call: layout calibration tests, then the tuned config-5 lines (twice)
+# one-off GPU call: rocprofv3 kernel stats of the secondary lines (decode_full, files, write14, repair12)
 set -o pipefail
 OUT=gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "layout or frames" > $OUT/pytest_layout.log 2>&1 || { tail -30 $OUT/pytest_layout.log; exit 1; }
-tail -2 $OUT/pytest_layout.log
-for r in 1 2; do
-for c in 262144 4194304 1048576 65536; do
-  timeout -k 10 300 python bench.py --workload mixed16 --chunk $c --layout tuned --steps 20 --no-cpu-baseline --no-host-inclusive > $OUT/tuned_line.json 2>> $OUT/tuned.err || { tail -20 $OUT/tuned.err; exit 1; }
-  cat $OUT/tuned_line.json >> $OUT/tuned2.jsonl
-  python3 -c "import json; d=json.load(open('$OUT/tuned_line.json')); print($c, d['roofline']['frac'], d['ops']['decode']['frac'], d['config']['layout'][:80])"
-done
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+for w in decode_full files write14 repair12; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof2_$w -o run --output-format csv -- \
+    python3 bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline --no-host-inclusive > $OUT/prof2_$w.json 2> $OUT/prof2_$w.err \
+    || { tail -20 $OUT/prof2_$w.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/prof2_$w.json')); print('$w', d['roofline']['avg_launch_ms'], d['roofline']['frac'])"
 done
