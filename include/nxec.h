@@ -206,8 +206,11 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * c*chunk_stride).  The batch layout is the caller's choice (every entry point
  * takes both strides); these strides avoid the DRAM channel/bank aliasing that
  * power-of-two chunk strides cause (profiles/r02_layout_*.log):
- *  - chunks >= 2 MiB: chunk_stride = len + 2 KiB (RS(16,4) 4 MiB: 0.71 -> 0.76
- *    of 8 TB/s, every erasure pattern >= 0.75);
+ *  - chunks >= 2 MiB: chunk_stride = len + a pad that breaks the
+ *    power-of-two stride: 3 KiB for multiples of 4 MiB (RS(16,4) 4 MiB: 0.71
+ *    packed, 0.754 with 2 KiB, 0.772 with 3 KiB of 8 TB/s, every erasure
+ *    pattern >= 0.76; RS(12,4) 4 MiB 0.756 -> 0.781), 5 KiB at 2 MiB, 2 KiB
+ *    otherwise;
  *  - stripes of 1 MiB-multiple chunks whose size is a power-of-two number of
  *    MiB: stripe_stride padded by one chunk to an odd multiple (RS(12,4) 1
  *    MiB: encode 0.80 -> 0.81, single-failure repair 0.74 -> 0.79);
@@ -227,7 +230,7 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * (equal weights; NXEC_LAYOUT_RECOVER_HEAVY doubles the scattered one) over a
  * scratch batch of about budget_bytes (<= 0: 24 GiB, capped at a quarter of
  * the free device memory) for a few candidate layouts (the table's, packed,
- * chunk pads of 2, 4 and 8 KiB, an odd stripe stride), each in two
+ * chunk pads of 1.5, 2, 3, 4, 5 and 8 KiB, an odd stripe stride), each in two
  * interleaved rounds; the table's layout stays unless another scores 0.5 %
  * higher.  The result is cached per (device, n, k, len, flags); the first
  * call for a shape takes ~0.5-2 s.  Uses ctx's

@@ -370,7 +370,11 @@ int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int6
     return set_error(NXEC_ERR_INVALID, "nxec_batch_layout: invalid arguments");
   constexpr int64_t kMiB = int64_t(1) << 20;
   int64_t cs = (len + 15) / 16 * 16;
-  if (len >= 2 * kMiB) cs += 2048;  // break the power-of-two chunk stride (profiles/r02_layout_sweep.log)
+  // break the power-of-two chunk stride (profiles/r02_layout_sweep.log; the
+  // pad per size class from r05_layout_big_pads.log, r05_config5_small_pads.log:
+  // 4 MiB multiples 3 KiB, e.g. RS(16,4) 4 MiB 0.754 -> 0.772, RS(12,4)
+  // 0.756 -> 0.781; 2 MiB 5 KiB; other sizes from 2 MiB 2 KiB)
+  if (len >= 2 * kMiB) cs += len % (4 * kMiB) == 0 ? 3072 : len == 2 * kMiB ? 5120 : 2048;
   int64_t ss = cs * n;
   // stripes of a power-of-two number of MiB alias worst: an odd multiple of
   // the chunk wins for every op there ((16,12) 1 MiB: encode 0.798 -> 0.812,
@@ -409,7 +413,8 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
   if ((rc = nxec_batch_layout(n, len, flags, &c0, &s0))) return rc;
   const int64_t packed = (len + 15) / 16 * 16;
   std::vector<std::pair<int64_t, int64_t>> cand = {{c0, s0}, {packed, n * packed}};
-  for (int64_t pad : {int64_t(2048), int64_t(4096), int64_t(8192)}) cand.emplace_back(packed + pad, n * (packed + pad));
+  for (int64_t pad : {int64_t(1536), int64_t(2048), int64_t(3072), int64_t(4096), int64_t(5120), int64_t(8192)})
+    cand.emplace_back(packed + pad, n * (packed + pad));
   cand.emplace_back(packed, (n + 1) * packed);  // an odd stripe stride in chunks
   std::sort(cand.begin() + 1, cand.end());
   cand.erase(std::unique(cand.begin() + 1, cand.end()), cand.end());

@@ -103,9 +103,10 @@ def test_arena_without_device_falls_back():
 
 def test_batch_layout_policy():
     """nxec_batch_layout (host-only arithmetic): chunk strides of >= 2 MiB
-    chunks padded by 2 KiB; stripes of a power-of-two number of MiB padded by
-    one chunk; any even number of MiB only when recover-heavy; 256 KiB and
-    64 KiB chunks left packed (profiles/r02_layout_sweep.log)."""
+    chunks padded (3 KiB for multiples of 4 MiB, 5 KiB at 2 MiB, 2 KiB
+    otherwise); stripes of a power-of-two number of MiB padded by one chunk;
+    any even number of MiB only when recover-heavy; 256 KiB and 64 KiB chunks
+    left packed (profiles/r02_layout_sweep.log, r05_layout_big_pads.log)."""
     M = 1 << 20
     assert nxec.batch_layout(14, M) == (M, 14 * M)
     assert nxec.batch_layout(14, M, 1) == (M, 15 * M)
@@ -115,7 +116,10 @@ def test_batch_layout_policy():
     assert nxec.batch_layout(20, 256 << 10) == (256 << 10, 20 * (256 << 10))
     assert nxec.batch_layout(15, M, 1) == (M, 15 * M)  # already odd
     cs, ss = nxec.batch_layout(20, 4 * M)
-    assert cs == 4 * M + 2048 and ss == 20 * cs
+    assert cs == 4 * M + 3072 and ss == 20 * cs
+    assert nxec.batch_layout(20, 8 * M)[0] == 8 * M + 3072
+    assert nxec.batch_layout(14, 2 * M)[0] == 2 * M + 5120
+    assert nxec.batch_layout(20, 3 * M)[0] == 3 * M + 2048
     for n, ln in [(14, M), (16, M), (20, 4 * M), (6, 3 * M + 5), (4, 2 * M)]:
         for fl in (0, 1):
             cs, ss = nxec.batch_layout(n, ln, fl)
