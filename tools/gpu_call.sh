@@ -1,7 +1,9 @@
-# one-off GPU call: the >= 2 MiB chunk pad (2 KiB today) against 3 / 5 / 6 / 7 KiB over geometries, twice
+# one-off GPU call: decode_full spread (three runs) beside the headline
 set -o pipefail
 OUT=gpurun_out
-PROBE_GIB=32 PROBE_REPEAT=2 PROBE_CPADS=2048,3072,5120,6144,7168 PROBE_SPADS=0 PROBE_SG=1 \
-  timeout -k 10 700 python3 -u tools/layout_probe.py 20,16,2048 20,16,8192 14,10,2048 14,10,4096 16,12,4096 12,8,4096 20,16,3072 \
-  > $OUT/bigpads.log 2>&1 || { tail -5 $OUT/bigpads.log; exit 1; }
-grep -c enc $OUT/bigpads.log
+for r in 1 2 3; do
+  timeout -k 10 300 python bench.py --workload decode_full --steps 10 --warmup 2 --no-cpu-baseline --no-host-inclusive > $OUT/df.json 2>> $OUT/df.err || { tail -20 $OUT/df.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/df.json')); print('decode_full', d['ms_per_step'], d['roofline']['frac'])"
+done
+timeout -k 10 300 python bench.py --steps 10 --no-cpu-baseline --no-host-inclusive > $OUT/hl.json 2>> $OUT/df.err || exit 1
+python3 -c "import json; d=json.load(open('$OUT/hl.json')); print('headline', d['value'], d['roofline']['frac'])"
