@@ -230,10 +230,10 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * (equal weights; NXEC_LAYOUT_RECOVER_HEAVY doubles the scattered one) over a
  * scratch batch of about budget_bytes (<= 0: 24 GiB, capped at a quarter of
  * the free device memory) for a few candidate layouts (the table's, packed,
- * chunk pads of 1.5, 2, 3, 4, 5 and 8 KiB, an odd stripe stride), each in two
+ * chunk pads of 1.5-16 KiB, an odd stripe stride), each in two
  * interleaved rounds; the table's layout stays unless another scores 0.5 %
  * higher.  The result is cached per (device, n, k, len, flags); the first
- * call for a shape takes ~0.5-2 s.  Uses ctx's
+ * call for a shape takes ~1-3 s.  Uses ctx's
  * stream and device; the scratch batch is freed before it returns. */
 int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
                             int64_t *chunk_stride, int64_t *stripe_stride);

@@ -413,7 +413,10 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
   if ((rc = nxec_batch_layout(n, len, flags, &c0, &s0))) return rc;
   const int64_t packed = (len + 15) / 16 * 16;
   std::vector<std::pair<int64_t, int64_t>> cand = {{c0, s0}, {packed, n * packed}};
-  for (int64_t pad : {int64_t(1536), int64_t(2048), int64_t(3072), int64_t(4096), int64_t(5120), int64_t(8192)})
+  // chunk pads: the 2-5 KiB class of the table, and the larger ones small
+  // chunks want ((14,10) 128 KiB: 0.68 packed, 0.78 with 10 KiB;
+  // profiles/r05_layout_small_chunk_pads.log)
+  for (int64_t pad : {1536, 2048, 3072, 4096, 5120, 8192, 10240, 12288, 16384})
     cand.emplace_back(packed + pad, n * (packed + pad));
   cand.emplace_back(packed, (n + 1) * packed);  // an odd stripe stride in chunks
   std::sort(cand.begin() + 1, cand.end());

@@ -1,9 +1,7 @@
-# one-off GPU call: decode_full spread (three runs) beside the headline
+# one-off GPU call: finer chunk pads at 128 / 256 / 512 KiB chunks over (14,10) and (20,16), twice
 set -o pipefail
 OUT=gpurun_out
-for r in 1 2 3; do
-  timeout -k 10 300 python bench.py --workload decode_full --steps 10 --warmup 2 --no-cpu-baseline --no-host-inclusive > $OUT/df.json 2>> $OUT/df.err || { tail -20 $OUT/df.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/df.json')); print('decode_full', d['ms_per_step'], d['roofline']['frac'])"
-done
-timeout -k 10 300 python bench.py --steps 10 --no-cpu-baseline --no-host-inclusive > $OUT/hl.json 2>> $OUT/df.err || exit 1
-python3 -c "import json; d=json.load(open('$OUT/hl.json')); print('headline', d['value'], d['roofline']['frac'])"
+PROBE_GIB=32 PROBE_REPEAT=2 PROBE_CPADS=0,1536,2560,3072,3584,4096,4608,5120,6144,7168,10240,12288 PROBE_SPADS=0 PROBE_SG=1 \
+  timeout -k 10 800 python3 -u tools/layout_probe.py 20,16,256 14,10,256 14,10,128 20,16,128 14,10,512 \
+  > $OUT/smallchunk_pads.log 2>&1 || { tail -5 $OUT/smallchunk_pads.log; exit 1; }
+grep -c enc $OUT/smallchunk_pads.log
