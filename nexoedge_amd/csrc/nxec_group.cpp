@@ -6,6 +6,7 @@
 // device thread runs on the CPUs of its GPU's NUMA node (nxec_numa.cpp), so
 // its staging copies and zero-copy PCIe traffic stay on that socket.
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -40,12 +41,21 @@ int run_all(nxec_group *g, F fn) {
   std::vector<int> rc(nd, NXEC_OK);
   std::vector<std::string> msg(nd);
   std::vector<std::thread> th;
-  for (int i = 0; i < nd; i++)
-    th.emplace_back([&, i] {
-      (void)nxec::bind_thread_cpus(g->cpus[i]);
-      rc[i] = fn(i);
-      if (rc[i] != NXEC_OK) msg[i] = nxec_last_error();
-    });
+  th.reserve(static_cast<size_t>(nd));
+  auto body = [&](int i) {
+    rc[i] = fn(i);
+    if (rc[i] != NXEC_OK) msg[i] = nxec_last_error();
+  };
+  for (int i = 0; i < nd; i++) {
+    try {
+      th.emplace_back([&, i] {
+        (void)nxec::bind_thread_cpus(g->cpus[i]);
+        body(i);
+      });
+    } catch (const std::system_error &) {
+      body(i);  // no thread to be had: this device's share on the calling thread
+    }
+  }
   for (auto &t : th) t.join();
   for (int i = 0; i < nd; i++)
     if (rc[i] != NXEC_OK) return nxec::set_error(rc[i], "device %d: %s", g->devices[i], msg[i].c_str());

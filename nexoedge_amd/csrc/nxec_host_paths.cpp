@@ -265,12 +265,15 @@ int start_request(const void *frames, int64_t nchunks, Fn &&fn, nxec_request_t *
   auto *r = new (std::nothrow) nxec_request();
   if (!r) return set_error(NXEC_ERR_NOMEM, "nxec request: out of memory");
   const auto *f = static_cast<unsigned char *const *>(frames);
-  r->frames.assign(f, f + nchunks);
   try {
+    r->frames.assign(f, f + nchunks);
     r->worker = std::thread([r, fn]() {
       r->rc = fn(r->frames.data());
       if (r->rc != NXEC_OK) r->error = last_error();
     });
+  } catch (const std::bad_alloc &) {
+    delete r;
+    return set_error(NXEC_ERR_NOMEM, "nxec request: out of memory");
   } catch (const std::system_error &) {
     delete r;
     return set_error(NXEC_ERR_HIP, "nxec request: cannot start a worker thread");
