@@ -1,6 +1,17 @@
-# one-off GPU call: L2 -> fabric latency / DRAM-credit counters for the headline geometry's recover
-# patterns (packed: contiguous vs scattered; odd stripe: scattered), 32 GiB passes
+# one-off GPU call: TA / TCP / TD counters of k_files_md5 over the alignment variants of
+# tools/files_align_probe.py (raw, a16, a16m, a4m, a8m; 1 warm + 3 timed launches each),
+# one counter group per pass
 set -o pipefail
-export PROBE_GIB=32
-STEPS="lat5" TCC_LAYOUTS="r10_packed_enc:14:10:1024:0:0:enc;r10_packed_rec0123:14:10:1024:0:0:0,1,2,3;r10_packed_rec_scat:14:10:1024:0:0:1,4,11,13;r10_odd_rec_scat:14:10:1024:0:1:1,4,11,13" \
-  bash tools/gpu_r05.sh
+OUT=gpurun_out
+ROOT=$PWD
+cd /tmp && export TMPDIR=/tmp
+export PROBE_REPS=3
+i=0
+for ctrs in "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
+            "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum" \
+            "TD_TD_BUSY_sum TD_TC_STALL_sum"; do
+  i=$((i+1))
+  timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv -d $ROOT/$OUT/fa_pmc/p$i -o run -- \
+    python3 $ROOT/tools/files_align_probe.py > $ROOT/$OUT/fa_pmc_p$i.log 2>&1 || { tail -5 $ROOT/$OUT/fa_pmc_p$i.log; exit 1; }
+done
+echo passes-done
