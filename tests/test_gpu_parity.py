@@ -1665,6 +1665,55 @@ def test_encode_objects_tail_inplace(gpu_ctx, n, k, M, nfiles):
     arena.free()
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_encode_objects_inplace_fuzz(gpu_ctx, seed):
+    """Seeded fuzz of the one-launch write with NXEC_OBJECTS_TAIL_INPLACE
+    (k_files_md5's masked chunks, zero line and page-end fallback): random
+    (n, k) up to 16 data chunks, chunk sizes 128 B - 32 KiB, 20-200 objects of
+    1 B - 3 stripes at random 16-byte aligned places, some ending 0-15 bytes
+    before a 4 KiB page boundary.  Parity and every digest equal the separate
+    launches' (pad copy + list coding + MD5 list), and each partial data
+    chunk's tail slot equals theirs (zero padded)."""
+    rng = np.random.default_rng(4242 + seed)
+    k = int(rng.integers(1, 17))
+    p = int(rng.integers(1, 5))
+    n, M = k + p, 16 * int(rng.integers(8, 2049))
+    nfiles = int(rng.integers(20, 201))
+    lengths = [int(x) for x in rng.integers(1, 3 * k * M + 1, size=nfiles)]
+    lengths[:3] = [k * M, 1, k * M + k * 16]  # a whole stripe, one byte, an exact short last stripe
+    offs, pos = [], 0
+    for L in lengths:
+        pos = (pos + 16 * int(rng.integers(0, 64)) + 15) // 16 * 16
+        if rng.random() < 0.3:  # end the object 0-15 bytes before a page boundary
+            end = (pos + L + 4095) // 4096 * 4096 - int(rng.integers(0, 16))
+            pos = max(pos, (end - L) // 16 * 16)
+        offs.append(pos)
+        pos += L
+    host = rng.integers(0, 256, size=pos + 64, dtype=np.uint8)
+    arena = up(host)
+    ptrs = [arena.ptr + o for o in offs]
+    pi, ti, mi = _encode_objects_out(gpu_ctx, n, k, M, ptrs, lengths, False, tail_fill=0xAB,
+                                     flags=nxec.OBJECTS_TAIL_INPLACE)
+    ps, ts, ms = _encode_objects_out(gpu_ctx, n, k, M, ptrs, lengths, True)
+    arena.free()
+    assert np.array_equal(mi, ms), (seed, n, k, M)
+    g, toff = 0, 0
+    for i, L in enumerate(lengths):
+        ns, nf, cl = nxec.object_layout(n, k, L, M)
+        for s in range(ns):
+            cs = M if s < nf else cl
+            assert np.array_equal(pi[g + s, :, :cs], ps[g + s, :, :cs]), (seed, i, s)
+        if ns > nf:
+            cls = (cl + 15) // 16 * 16
+            rem = L - nf * k * M
+            jf, part = rem // cl, rem % cl
+            if part:
+                a, b = toff + jf * cls, toff + (jf + 1) * cls
+                assert np.array_equal(ti[a:b], ts[a:b]), (seed, i, jf)
+            toff += k * cls
+        g += ns
+
+
 @pytest.mark.parametrize("flags", [0, "inplace"])
 def test_encode_objects_last_stripe_at_a_page_end(gpu_ctx, flags):
     """Last stripes read in place (k_files_md5's masked chunk) never touch a
