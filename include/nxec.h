@@ -211,6 +211,9 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  *    packed, 0.754 with 2 KiB, 0.772 with 3 KiB of 8 TB/s, every erasure
  *    pattern >= 0.76; RS(12,4) 4 MiB 0.756 -> 0.781), 5 KiB at 2 MiB, 2 KiB
  *    otherwise;
+ *  - measured smaller shapes: n = 20 with 256 KiB chunks +4 KiB (RS(16,4)
+ *    0.755 -> 0.766), n = 14 with 128 KiB +10 KiB (0.68 -> 0.78) and 256
+ *    KiB +12 KiB (0.71 -> 0.745); other small shapes: nxec_batch_layout_tuned;
  *  - stripes of 1 MiB-multiple chunks whose size is a power-of-two number of
  *    MiB: stripe_stride padded by one chunk to an odd multiple (RS(12,4) 1
  *    MiB: encode 0.80 -> 0.81, single-failure repair 0.74 -> 0.79);

@@ -375,6 +375,20 @@ int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int6
   // 4 MiB multiples 3 KiB, e.g. RS(16,4) 4 MiB 0.754 -> 0.772, RS(12,4)
   // 0.756 -> 0.781; 2 MiB 5 KiB; other sizes from 2 MiB 2 KiB)
   if (len >= 2 * kMiB) cs += len % (4 * kMiB) == 0 ? 3072 : len == 2 * kMiB ? 5120 : 2048;
+  // smaller chunks: no rule carries across geometries, so only the shapes
+  // measured (mean of encode and the contiguous / scattered recovers,
+  // profiles/r05_config5_small_pads.log, r05_layout_small_chunk_pads.log)
+  struct Measured {
+    int n;
+    int64_t len, pad;
+  };
+  static constexpr Measured kMeasured[] = {
+      {20, 256 << 10, 4096},   // RS(16,4) 256 KiB: 0.755 -> 0.766
+      {14, 128 << 10, 10240},  // RS(10,4) 128 KiB: 0.68 -> 0.78
+      {14, 256 << 10, 12288},  // RS(10,4) 256 KiB: 0.71 -> 0.745
+  };
+  for (const Measured &m : kMeasured)
+    if (n == m.n && len == m.len) cs += m.pad;
   int64_t ss = cs * n;
   // stripes of a power-of-two number of MiB alias worst: an odd multiple of
   // the chunk wins for every op there ((16,12) 1 MiB: encode 0.798 -> 0.812,

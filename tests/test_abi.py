@@ -105,15 +105,19 @@ def test_batch_layout_policy():
     """nxec_batch_layout (host-only arithmetic): chunk strides of >= 2 MiB
     chunks padded (3 KiB for multiples of 4 MiB, 5 KiB at 2 MiB, 2 KiB
     otherwise); stripes of a power-of-two number of MiB padded by one chunk;
-    any even number of MiB only when recover-heavy; 256 KiB and 64 KiB chunks
-    left packed (profiles/r02_layout_sweep.log, r05_layout_big_pads.log)."""
+    any even number of MiB only when recover-heavy; three measured small
+    shapes padded, other small chunks packed (profiles/r02_layout_sweep.log,
+    r05_layout_big_pads.log, r05_layout_small_chunk_pads.log)."""
     M = 1 << 20
     assert nxec.batch_layout(14, M) == (M, 14 * M)
     assert nxec.batch_layout(14, M, 1) == (M, 15 * M)
     assert nxec.batch_layout(16, M) == (M, 17 * M)
     assert nxec.batch_layout(20, M) == (M, 20 * M)
     assert nxec.batch_layout(20, M, 1) == (M, 21 * M)
-    assert nxec.batch_layout(20, 256 << 10) == (256 << 10, 20 * (256 << 10))
+    assert nxec.batch_layout(20, 256 << 10) == ((256 << 10) + 4096, 20 * ((256 << 10) + 4096))  # measured shapes
+    assert nxec.batch_layout(14, 128 << 10)[0] == (128 << 10) + 10240
+    assert nxec.batch_layout(14, 256 << 10)[0] == (256 << 10) + 12288
+    assert nxec.batch_layout(16, 256 << 10) == (256 << 10, 16 * (256 << 10))  # not measured: packed
     assert nxec.batch_layout(15, M, 1) == (M, 15 * M)  # already odd
     cs, ss = nxec.batch_layout(20, 4 * M)
     assert cs == 4 * M + 3072 and ss == 20 * cs
