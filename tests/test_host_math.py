@@ -159,3 +159,17 @@ def test_every_tool_is_cited():
     text += "".join(open(os.path.join(tdir, f)).read() for f in os.listdir(tdir) if f.endswith(".py"))
     missing = [e for e in entries if f"tools/{e}" not in text]
     assert not missing, missing
+
+
+def test_every_cited_profile_exists():
+    """Every profiles/rNN_* file DESIGN.md, README.md or INTEGRATION.md cites
+    is committed (the evidence the text quotes is there to be checked)."""
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = "".join(open(os.path.join(root, f)).read() for f in ("DESIGN.md", "README.md", "INTEGRATION.md"))
+    names = set(re.findall(r"\b(r0[1-9]_[A-Za-z0-9_\-.]+?\.(?:jsonl|json|log|csv|txt))(?![A-Za-z0-9])", text))
+    assert len(names) > 100
+    missing = sorted(n for n in names if not os.path.exists(os.path.join(root, "profiles", n)))
+    assert not missing, missing
+
