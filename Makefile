@@ -22,7 +22,7 @@ LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))
 HDRS     := include/nxec.h $(CSRC)/nxec_internal.h $(CSRC)/nxec_runtime.h $(CSRC)/nxec_tuning.h $(CSRC)/nxec_device.h $(CSRC)/nxec_em_common.h $(wildcard $(CSRC)/coding/*.hh)
 
 all: $(LIBDIR)/libnxec.so oracle/liboracle.so build/rs_surface_test build/isal_compat_test build/chunk_manager_flow_test \
-     build/stripe_batch_test build/chunk_replay_test
+     build/stripe_batch_test build/chunk_replay_test build/dropin_pool_test
 
 # rs.cc's ISA-L call sequence compiled against include/nxec_isal_compat.h (plain C)
 build/isal_compat_test: tests/cpp/isal_compat_test.c include/nxec_isal_compat.h $(LIBDIR)/libnxec.so
@@ -38,6 +38,13 @@ build/rs_surface_test: tests/cpp/rs_surface_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 build/stripe_batch_test: tests/cpp/stripe_batch_test.cc $(LIBDIR)/libnxec.so $(HDRS)
 	@mkdir -p build
 	g++ -std=c++17 -O2 -Wall -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lcrypto -o $@
+
+# the default pool under 16 proxy workers sharing one RSCode (oracle = checker only)
+build/dropin_pool_test: tests/cpp/dropin_pool_test.cc $(LIBDIR)/libnxec.so oracle/liboracle.so $(HDRS)
+	@mkdir -p build
+	g++ -std=c++17 -O2 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -I$(CSRC) $< -L$(LIBDIR) -lnxec \
+	    -Loracle -loracle -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,'$$ORIGIN/../oracle' \
+	    -Wl,-rpath,/opt/rocm/lib -lcrypto -lpthread -o $@
 
 # the reference's Chunk ownership sequences (shallow copies + freeData = false)
 build/chunk_replay_test: tests/cpp/chunk_replay_test.cc $(LIBDIR)/libnxec.so $(HDRS)

@@ -752,8 +752,9 @@ def group_measure(args):
     hipSetDevice + streams per GPU"): an nxec_group of N contexts, member i
     owning its own args.stripes-stripe batch on device i (weak scaling, as the
     ranks), each step the headline's encode + recover (rotating patterns)
-    through nxec_group_rs_{encode,recover}_stripes -- one host thread per
-    member per call, every call synchronous.  Verified as the ranks' run: the
+    through nxec_group_rs_{encode,recover}_stripes_async -- each member's
+    long-lived thread queues both launches on its stream, one nxec_group_wait
+    per step (the ranks' pattern).  Verified as the ranks' run: the
     batches' checksums survive the timed steps, and erased chunks of every
     member come back.  Aggregate user-visible GiB/s of all members."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
@@ -779,9 +780,10 @@ def group_measure(args):
             out.append(b.checksum())
         return out
 
-    def step(i):
-        g.rs_encode(n, k, ptrs, cst, stripe, cs, counts)
-        g.rs_recover(n, k, PATTERNS[i % len(PATTERNS)], ptrs, cst, stripe, cs, counts)
+    def step(i):  # queued on every member's thread and stream; one wait per step, as the ranks
+        g.rs_encode_async(n, k, ptrs, cst, stripe, cs, counts)
+        g.rs_recover_async(n, k, PATTERNS[i % len(PATTERNS)], ptrs, cst, stripe, cs, counts)
+        g.wait()
 
     for i in range(max(1, args.warmup)):
         step(i)
@@ -808,7 +810,8 @@ def group_measure(args):
     return {"value": round(step_bytes * args.steps / dt / GIB, 2), "unit": "GiB/s", "members": len(devices),
             "devices": devices, "stripes_per_member": ns, "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "verified": verified, "layout": lay,
-            "note": "one process, nxec_group: a host thread + context per member, each call synchronous; "
+            "note": "one process, nxec_group: a long-lived host thread + context per member, encode + recover "
+                    "queued per step, one group wait; "
                     "encode (k+p)*cs + recover (k+e)*cs per stripe as the headline"}
 
 

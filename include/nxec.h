@@ -68,8 +68,8 @@ void nxec_ec_init_tables(int k, int rows, unsigned char *a, unsigned char *gftbl
  * 2. Drop-in synchronous host-buffer encode -- replaces ISA-L ec_encode_data
  *    (erasure_code.h:98) at rs.cc:89,106,230 and coding_util.hh:21,28.
  *    coding[r][i] = XOR_j c(r,j) * data[j][i], c from gftbls (byte [1]).
- *    Runs on the calling thread's current device (a per-device default
- *    context), staging through pinned memory.  The ISA-L signature has no
+ *    Runs on a context of the default pool (below), staging through pinned
+ *    memory.  The ISA-L signature has no
  *    error channel: on a device error the void form retries once on a fresh
  *    context through the plain staged path (H2D, multiply, D2H), and aborts
  *    with a message only when that fails too (or the arguments are invalid) --
@@ -83,6 +83,34 @@ int nxec_ec_encode_data_status(int len, int k, int rows, const unsigned char *gf
 /* same, taking the rows x k coefficient matrix directly (no 32-B tables) */
 int nxec_encode_host(int len, int k, int rows, const unsigned char *coeffs, const unsigned char *const *data,
                      unsigned char *const *coding);
+
+/* The default pool: the contexts the entry points without a context argument
+ * (this section: nxec_ec_encode_data, nxec_encode_host*, and RSCode /
+ * CodingUtils through them) run on.  An unmodified proxy never selects a GPU
+ * and shares one RSCode across its worker threads (chunk_manager.cc:
+ * 1779-1801, zmq.cc:83), so each call leases the member nxec_default_pick
+ * chooses and makes that member's device current for the call only (the
+ * caller's current device is restored on return).
+ *   devices = NULL, n = 0: one context per visible device (the default);
+ *   n < 0: the calling thread's current device (the single-device rule of
+ *          rounds 1-5);
+ *   n > 0: the listed devices, one context per entry (a device listed twice
+ *          gets two contexts).
+ * Deployment setting NXEC_DEFAULT_DEVICES=all|current|<d,d,...> (read at the
+ * first call; this function overrides it).  Contexts of earlier members stay
+ * alive; calls in flight finish on the member they leased. */
+int nxec_default_devices(const int *devices, int n);
+/* The pool's members (up to max): device, NUMA node of its PCIe root (-1
+ * unknown), calls served, calls in flight; *count = members.  With the
+ * `current` rule: every device a call has used. */
+int nxec_default_pool_stats(int *devices, int *nodes, unsigned long long *calls, int *inflight, int max, int *count);
+/* The per-call choice among n members: the fewest calls in flight, where a
+ * member on another NUMA node than the calling CPU's (caller_node; -1 or a
+ * node of -1: unknown, no preference) counts half a call more -- a local
+ * device wins ties, a remote one is taken only when it has fewer calls in
+ * flight; on an exact tie `prev` (the member this thread used last; -1
+ * none), else the lowest index.  Pure (no device); returns the index. */
+int nxec_default_pick(int n, const int *inflight, const int *nodes, int caller_node, int prev);
 
 /* nxec_encode_host plus fused pass-through: for j < k with copy_idx[j] >= 0,
  * data[j] is also delivered to copy_out[copy_idx[j]] by the same GPU pass
@@ -233,13 +261,22 @@ int nxec_rs_decode_stripes(nxec_ctx_t *ctx, int n, int k, const int32_t *failed,
  * (equal weights; NXEC_LAYOUT_RECOVER_HEAVY doubles the scattered one) over a
  * scratch batch of about budget_bytes (<= 0: 24 GiB, capped at a quarter of
  * the free device memory) for a few candidate layouts (the table's, packed,
- * chunk pads of 1.5-16 KiB, an odd stripe stride), each in two
- * interleaved rounds; the table's layout stays unless another scores 0.5 %
- * higher.  The result is cached per (device, n, k, len, flags); the first
- * call for a shape takes ~1-3 s.  Uses ctx's
+ * chunk pads of 1.5-16 KiB, an odd stripe stride), each in three
+ * interleaved rounds; the table's layout stays unless another beats it in
+ * every round by more than the rounds' spread (nxec_layout_choose, at least
+ * 0.5 %).  The result is cached per (device, n, k, len, flags, budget_bytes);
+ * the first call for a shape takes ~2-4 s.  Uses ctx's
  * stream and device; the scratch batch is freed before it returns. */
 int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
                             int64_t *chunk_stride, int64_t *stripe_stride);
+/* The choice rule of nxec_batch_layout_tuned (pure; exported for tests):
+ * scores[r * ncand + c] = candidate c's score in round r (c = 0 is the
+ * incumbent, the table's layout; <= 0 = not measured).  A challenger replaces
+ * the incumbent only when it beats it in EVERY round by more than
+ * max(min_margin, the relative spread (max - min) / mean of its own and the
+ * incumbent's scores across the rounds); among such challengers the highest
+ * mean wins.  Otherwise (ties included) 0: the incumbent. */
+int nxec_layout_choose(int ncand, int rounds, const double *scores, double min_margin);
 int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int64_t *stripe_stride);
 
 /* Host-resident batch encode (the proxy write path): h_data [s][k][len] in,
@@ -535,8 +572,10 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
 
 /* ---- Multi-GPU group in one process: one context per device,
  * a batch's stripes split into contiguous ranges (sizes differ by at most one),
- * one host thread per device; no collective, no peer traffic.  Calls are
- * synchronous.  A device may appear twice (two contexts on one GPU). */
+ * one long-lived host thread per member (started by nxec_group_create, bound
+ * once to its GPU's NUMA node); no collective, no peer traffic.  The plain
+ * calls are synchronous; the _async forms below are not.  A device may appear
+ * twice (two contexts on one GPU). */
 typedef struct nxec_group nxec_group_t;
 int nxec_group_create(const int *devices, int ndevices, nxec_group_t **out);
 void nxec_group_destroy(nxec_group_t *g);
@@ -554,6 +593,19 @@ int nxec_group_rs_encode_stripes(nxec_group_t *g, int n, int k, unsigned char *c
 int nxec_group_rs_recover_stripes(nxec_group_t *g, int n, int k, const int32_t *failed, int nfailed,
                                   unsigned char *const *d_stripes, int64_t chunk_stride, int64_t stripe_stride,
                                   int64_t len, const int64_t *nstripes);
+/* Asynchronous forms: each member's thread queues its shard's launches on its
+ * context's stream and the call returns at once (the arrays are copied; a
+ * member runs its calls in submission order).  Per-member failures (bad
+ * arguments of one member's shard, a launch error) are kept and returned by
+ * the next nxec_group_wait, which blocks until every call queued before it
+ * has finished on every member's device. */
+int nxec_group_rs_encode_stripes_async(nxec_group_t *g, int n, int k, unsigned char *const *d_stripes,
+                                       int64_t chunk_stride, int64_t stripe_stride, int64_t len,
+                                       const int64_t *nstripes);
+int nxec_group_rs_recover_stripes_async(nxec_group_t *g, int n, int k, const int32_t *failed, int nfailed,
+                                        unsigned char *const *d_stripes, int64_t chunk_stride, int64_t stripe_stride,
+                                        int64_t len, const int64_t *nstripes);
+int nxec_group_wait(nxec_group_t *g);
 
 /* ---------------------------------------------------------------------------
  * 5. Device plumbing (memory, streams, events) so hosts without a GPU

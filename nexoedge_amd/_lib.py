@@ -46,6 +46,9 @@ _PROTOS = {
     "nxec_encode_host": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp]),
     "nxec_encode_host_ex": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "nxec_encode_host_md5": (C.c_int, [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
+    "nxec_default_devices": (C.c_int, [vp, C.c_int]),
+    "nxec_default_pool_stats": (C.c_int, [vp, vp, vp, vp, C.c_int, vp]),
+    "nxec_default_pick": (C.c_int, [C.c_int, vp, vp, C.c_int, C.c_int]),
     "nxec_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
     "nxec_ctx_destroy": (None, [vp]),
     "nxec_ctx_stream": (vp, [vp]),
@@ -155,6 +158,10 @@ _PROTOS = {
     "nxec_group_rs_encode_host_batch": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, i64, i64, i64]),
     "nxec_group_rs_encode_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, vp]),
     "nxec_group_rs_recover_stripes": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, vp]),
+    "nxec_group_rs_encode_stripes_async": (C.c_int, [vp, C.c_int, C.c_int, vp, i64, i64, i64, vp]),
+    "nxec_group_rs_recover_stripes_async": (C.c_int, [vp, C.c_int, C.c_int, vp, C.c_int, vp, i64, i64, i64, vp]),
+    "nxec_group_wait": (C.c_int, [vp]),
+    "nxec_layout_choose": (C.c_int, [C.c_int, C.c_int, vp, C.c_double]),
 }
 
 

@@ -81,7 +81,7 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
     const uint8_t *dg = b.slot->h + b.md5_off + i * size_t(nh) * 16;
     if (o == 0 && r.md5) std::memcpy(r.md5, dg + size_t(b.hsrc) * 16, size_t(no) * 16);
     if (o == 0 && r.md5_inputs && b.hsrc) std::memcpy(r.md5_inputs, dg, size_t(b.hsrc) * 16);
-  });
+  }, HostLane::kOut);
   b.reqs.clear();
   return NXEC_OK;
 }

@@ -19,6 +19,8 @@
 #include <thread>
 #include <vector>
 
+#include <sched.h>
+
 #include "nxec_runtime.h"
 
 namespace nxec {
@@ -67,9 +69,17 @@ namespace {
 // the calling thread works too, and concurrent callers share the pool.
 class HostPool {
  public:
-  static HostPool &get() {
-    static HostPool pool;
-    return pool;
+  // With the lanes probe on (nxec_tuning.h host_lanes) copies into pinned
+  // staging and copies out of it have a worker set each, so a pipelined
+  // caller's gather and scatter (nxec_decode_frames) do not queue behind each
+  // other's helper tasks; otherwise one shared pool (rounds 1-5).
+  static HostPool &get(HostLane lane) {
+    static HostPool in;
+    if (lane == HostLane::kOut && tuning().host_lanes) {
+      static HostPool out;
+      return out;
+    }
+    return in;
   }
   // runs fn(i) for i in [0, n), returns when all are done.  The pool serves
   // two jobs at a time (a pipelined caller's gather and scatter,
@@ -186,7 +196,9 @@ void *host_device_view_range(const void *h, size_t bytes) {
   return d0;
 }
 
-void host_parallel_for(int n, const std::function<void(int)> &fn) { HostPool::get().parallel_for(n, fn); }
+void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane) {
+  HostPool::get(lane).parallel_for(n, fn);
+}
 
 int set_error(int code, const char *fmt, ...) {
   char buf[512];
@@ -373,29 +385,197 @@ int batch_stage(nxec_ctx_t *ctx, size_t slot_bytes, std::unique_lock<std::mutex>
   return NXEC_OK;
 }
 
+// ---- The default-context pool of the entry points that take no context ----
+// The reference shares one RSCode across the proxy's worker threads
+// (chunk_manager.cc:1779-1801, zmq.cc:83) and never selects a GPU, so the
+// drop-in cannot follow "the caller's device": every stripe would go to
+// device 0 over one PCIe link.  Instead each call leases a member of a pool --
+// by default one context per visible device -- chosen per call by
+// nxec_default_pick: the member with the fewest calls in flight, a device on
+// the calling CPU's NUMA node winning ties against a remote one by one call
+// (a remote device is taken only when it has fewer calls in flight than the
+// local one), and on an exact tie the member this thread used last (its
+// staging slots are warm).  NXEC_DEFAULT_DEVICES=current keeps the old rule
+// (the calling thread's current device); a list ("0,0,1") names the members,
+// a device listed twice getting two contexts.  Members' contexts live for the
+// process: a reconfiguration (nxec_default_devices) only changes which serve.
 namespace {
-std::mutex g_default_mu;
-std::vector<nxec_ctx_t *> g_default_ctx;
+
+struct Member {
+  int device = 0, ordinal = 0, node = -1;
+  std::mutex mu;  // creation of ctx
+  std::atomic<nxec_ctx_t *> ctx{nullptr};
+  std::atomic<int> inflight{0};
+  std::atomic<unsigned long long> calls{0};
+};
+
+struct PoolCfg {
+  bool current = false;           // the calling thread's current device
+  std::vector<Member *> members;  // list mode
+  uint64_t gen = 0;
+};
+
+std::mutex g_pool_mu;
+std::deque<Member> g_members;                 // every member ever made (stable addresses)
+std::shared_ptr<const PoolCfg> g_pool;        // null: not resolved yet
+std::vector<int> g_pool_request;              // nxec_default_devices' list (resolved at next use)
+int g_pool_request_mode = -2;                 // -2 unset (environment), -1 current, 0 all, 1 list
+uint64_t g_pool_gen = 0;
+thread_local int t_prev_member = -1;
+thread_local uint64_t t_prev_gen = 0;
+
+// under g_pool_mu: the member for (device, ordinal), made on first use
+Member *member_for(int device, int ordinal) {
+  for (Member &m : g_members)
+    if (m.device == device && m.ordinal == ordinal) return &m;
+  g_members.emplace_back();
+  Member &m = g_members.back();
+  m.device = device;
+  m.ordinal = ordinal;
+  char bus[64] = {0};
+  int node = -1;
+  if (device_bus_id(device, bus, sizeof(bus)) == NXEC_OK) (void)pci_node_cpus(bus, &node);
+  m.node = node;
+  return &m;
+}
+
+// "all" | "current" | "0,0,1" -> mode (-1 current, 0 all, 1 list) and list; false when malformed
+bool parse_devices(const char *text, int *mode, std::vector<int> *devs) {
+  devs->clear();
+  const std::string t(text);
+  if (t.empty() || t == "all") {
+    *mode = 0;
+    return true;
+  }
+  if (t == "current") {
+    *mode = -1;
+    return true;
+  }
+  size_t i = 0;
+  while (i < t.size()) {
+    size_t j = t.find(',', i);
+    if (j == std::string::npos) j = t.size();
+    const std::string f = t.substr(i, j - i);
+    char *end = nullptr;
+    const long d = std::strtol(f.c_str(), &end, 10);
+    if (f.empty() || *end != '\0' || d < 0 || d > 4095) return false;
+    devs->push_back(static_cast<int>(d));
+    i = j + 1;
+  }
+  *mode = 1;
+  return !devs->empty();
+}
+
+// under g_pool_mu
+int resolve_pool(std::shared_ptr<const PoolCfg> *out) {
+  if (!g_pool) {
+    int mode = g_pool_request_mode;
+    std::vector<int> devs = g_pool_request;
+    if (mode == -2) {  // deployment setting NXEC_DEFAULT_DEVICES
+      const char *e = std::getenv("NXEC_DEFAULT_DEVICES");
+      if (!parse_devices(e ? e : "all", &mode, &devs))
+        return set_error(NXEC_ERR_INVALID, "NXEC_DEFAULT_DEVICES=%s: expected all, current or a device list", e);
+    }
+    auto cfg = std::make_shared<PoolCfg>();
+    cfg->gen = ++g_pool_gen;
+    cfg->current = mode == -1;
+    if (mode == 0) {
+      int count = 0;
+      const hipError_t e = hipGetDeviceCount(&count);
+      if (e != hipSuccess || count == 0) {
+        (void)hipGetLastError();
+        return set_error(NXEC_ERR_NODEV, "no HIP device available (%s)", hipGetErrorString(e));
+      }
+      for (int d = 0; d < count; d++) devs.push_back(d);
+    }
+    if (mode >= 0) {
+      std::vector<int> seen;
+      for (int d : devs) {
+        const int ord = static_cast<int>(std::count(seen.begin(), seen.end(), d));
+        seen.push_back(d);
+        cfg->members.push_back(member_for(d, ord));
+      }
+    }
+    g_pool = cfg;
+  }
+  *out = g_pool;
+  return NXEC_OK;
+}
+
+int member_ctx(Member *m, nxec_ctx_t **out) {
+  nxec_ctx_t *c = m->ctx.load(std::memory_order_acquire);
+  if (!c) {
+    std::lock_guard<std::mutex> lk(m->mu);
+    c = m->ctx.load(std::memory_order_acquire);
+    if (!c) {
+      if (int rc = nxec_ctx_create(m->device, &c)) return rc;
+      m->ctx.store(c, std::memory_order_release);
+    }
+  }
+  *out = c;
+  return NXEC_OK;
+}
+
 }  // namespace
 
-int default_ctx(nxec_ctx_t **out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return hip_err(e, "hipGetDevice");
-  std::lock_guard<std::mutex> lk(g_default_mu);
-  if (g_default_ctx.size() <= static_cast<size_t>(dev)) g_default_ctx.resize(dev + 1, nullptr);
-  if (!g_default_ctx[dev]) {
-    int rc = nxec_ctx_create(dev, &g_default_ctx[dev]);
-    if (rc) return rc;
+DefaultLease::~DefaultLease() {
+  if (member_) static_cast<Member *>(member_)->inflight.fetch_sub(1, std::memory_order_relaxed);
+  int cur = -1;
+  if (saved_device_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != saved_device_) (void)hipSetDevice(saved_device_);
+}
+
+int default_ctx(DefaultLease &lease) {
+  std::shared_ptr<const PoolCfg> cfg;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (int rc = resolve_pool(&cfg)) return rc;
   }
-  *out = g_default_ctx[dev];
+  int saved = 0;
+  hipError_t e = hipGetDevice(&saved);
+  if (e != hipSuccess) return hip_err(e, "hipGetDevice");
+  Member *m = nullptr;
+  if (cfg->current) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    m = member_for(saved, 0);
+  } else {
+    const int n = static_cast<int>(cfg->members.size());
+    std::vector<int> inflight(n), nodes(n);
+    for (int i = 0; i < n; i++) {
+      inflight[i] = cfg->members[i]->inflight.load(std::memory_order_relaxed);
+      nodes[i] = cfg->members[i]->node;
+    }
+    const int prev = t_prev_gen == cfg->gen ? t_prev_member : -1;
+    const int idx = nxec_default_pick(n, inflight.data(), nodes.data(), cpu_numa_node(sched_getcpu()), prev);
+    m = cfg->members[idx];
+    t_prev_member = idx;
+    t_prev_gen = cfg->gen;
+  }
+  m->inflight.fetch_add(1, std::memory_order_relaxed);
+  m->calls.fetch_add(1, std::memory_order_relaxed);
+  lease.member_ = m;
+  lease.saved_device_ = saved;
+  nxec_ctx_t *c = nullptr;
+  if (int rc = member_ctx(m, &c)) return rc;
+  lease.ctx = c;
+  // this call runs on c's device (the lease restores the caller's on release)
+  if (int rc = ensure_device(c->device)) return rc;
+  // calls in flight on the device: its PCIe link's share (zero copy or DMA)
+  int dev_inflight = 0;
+  if (cfg->current) {
+    dev_inflight = m->inflight.load(std::memory_order_relaxed);
+  } else {
+    for (Member *o : cfg->members)
+      if (o->device == m->device) dev_inflight += o->inflight.load(std::memory_order_relaxed);
+  }
+  lease.device_inflight = std::max(1, dev_inflight);
   return NXEC_OK;
 }
 
 int zero_line(nxec_ctx_t *ctx, size_t bytes, const uint8_t **out) {
   std::lock_guard<std::mutex> lk(ctx->zero_mu);
   if (ctx->zero_bytes < bytes) {
-    const size_t want = std::max<size_t>((bytes + 4095) / 4096 * 4096, size_t(1) << 20);
+    // at least doubling, so a context retires few lines however its callers' sizes creep up
+    const size_t want = std::max<size_t>({(bytes + 4095) / 4096 * 4096, size_t(1) << 20, 2 * ctx->zero_bytes});
     uint8_t *z = nullptr;
     NXEC_HIP(hipMalloc(reinterpret_cast<void **>(&z), want));
     hipError_t e = hipMemsetAsync(z, 0, want, ctx->stream);
@@ -404,11 +584,11 @@ int zero_line(nxec_ctx_t *ctx, size_t bytes, const uint8_t **out) {
       (void)hipFree(z);
       return hip_err(e, "zero line");
     }
-    // the old line may still be read by queued launches on other streams
-    if (ctx->zero) {
-      (void)hipDeviceSynchronize();
-      (void)hipFree(ctx->zero);
-    }
+    // Launches queued (or about to be queued: a caller that took the old line
+    // and has not launched yet) may still read the old line, so it is retired,
+    // never freed while the context lives (nxec_ctx_destroy frees it).  Lines
+    // at least double, so a context holds about log2(M / 1 MiB) + 1 of them.
+    if (ctx->zero) ctx->zero_retired.push_back(ctx->zero);
     ctx->zero = z;
     ctx->zero_bytes = want;
   }
@@ -444,10 +624,6 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   ctx->obj.release();  // before the context stream it borrows
-  if (ctx->zero) {
-    (void)hipDeviceSynchronize();
-    (void)hipFree(ctx->zero);
-  }
   for (auto &pr : ctx->kt_pending) {
     (void)hipEventSynchronize(pr.second);
     (void)hipEventDestroy(pr.first);
@@ -457,6 +633,10 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
   }
+  // the zero lines last: launches on the context's streams have drained above
+  // (hipFree itself waits for the device)
+  if (ctx->zero) ctx->zero_retired.push_back(ctx->zero);
+  for (uint8_t *z : ctx->zero_retired) (void)hipFree(z);
   for (Slot *s : ctx->all_slots) {
     if (s->stream) {
       (void)hipStreamSynchronize(s->stream);
@@ -475,6 +655,53 @@ void nxec_ctx_destroy(nxec_ctx_t *ctx) {
 }
 
 void *nxec_ctx_stream(nxec_ctx_t *ctx) { return ctx ? static_cast<void *>(ctx->stream) : nullptr; }
+
+int nxec_default_pick(int n, const int *inflight, const int *nodes, int caller_node, int prev) {
+  if (n < 1 || !inflight) return set_error(NXEC_ERR_INVALID, "nxec_default_pick: invalid arguments");
+  int best = -1;
+  long best_cost = 0;
+  for (int i = 0; i < n; i++) {
+    const bool remote = nodes && caller_node >= 0 && nodes[i] >= 0 && nodes[i] != caller_node;
+    const long cost = 2L * std::max(0, inflight[i]) + (remote ? 1 : 0);
+    if (best < 0 || cost < best_cost || (cost == best_cost && i == prev)) {
+      best = i;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+int nxec_default_devices(const int *devices, int n) {
+  if (n > 0 && !devices) return set_error(NXEC_ERR_INVALID, "nxec_default_devices: null device list");
+  for (int i = 0; i < n; i++)
+    if (devices[i] < 0) return set_error(NXEC_ERR_INVALID, "nxec_default_devices: device %d", devices[i]);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool_request_mode = n < 0 ? -1 : (n == 0 ? 0 : 1);
+  g_pool_request.clear();
+  if (n > 0) g_pool_request.assign(devices, devices + n);
+  g_pool.reset();  // resolved at the next call; calls in flight keep their snapshot
+  return NXEC_OK;
+}
+
+int nxec_default_pool_stats(int *devices, int *nodes, unsigned long long *calls, int *inflight, int max, int *count) {
+  if (!count || (max > 0 && (!devices || !nodes || !calls || !inflight)))
+    return set_error(NXEC_ERR_INVALID, "nxec_default_pool_stats: invalid arguments");
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  std::vector<Member *> ms;
+  if (g_pool && !g_pool->current) {
+    ms = g_pool->members;
+  } else {
+    for (Member &m : g_members) ms.push_back(&m);  // current mode: every device used so far
+  }
+  *count = static_cast<int>(ms.size());
+  for (int i = 0; i < max && i < *count; i++) {
+    devices[i] = ms[i]->device;
+    nodes[i] = ms[i]->node;
+    calls[i] = ms[i]->calls.load(std::memory_order_relaxed);
+    inflight[i] = ms[i]->inflight.load(std::memory_order_relaxed);
+  }
+  return NXEC_OK;
+}
 
 }  // extern "C"
 

@@ -31,10 +31,6 @@ struct DigestJob {
 
 namespace {
 
-// host entry-point calls in flight (the pipelined, pool-assisted form is for
-// few callers; many concurrent callers are better served one piece each)
-std::atomic<int> g_host_calls{0};
-
 constexpr int kNotPinned = 1;  // encode_host_pinned: some input is not device-mapped
 
 // nxec_encode_host whose inputs are all pinned / registered host memory
@@ -104,9 +100,11 @@ int encode_host_pinned(nxec_ctx_t *ctx, int len, int k, int rows, const unsigned
   const hipError_t e = hipStreamSynchronize(st);  // the slot goes back only once drained
   if (!rc) rc = hip_check(e, "encode_host (pinned) sync");
   if (!rc && staged)
-    host_parallel_for(rows, [&](int r) {
-      if (!out_mapped[r]) std::memcpy(coding[r], slot->h + chunk_off(k + r), size_t(len));
-    });
+    host_parallel_for(
+        rows, [&](int r) {
+          if (!out_mapped[r]) std::memcpy(coding[r], slot->h + chunk_off(k + r), size_t(len));
+        },
+        HostLane::kOut);
   release_slot(ctx, slot);
   return rc;
 }
@@ -124,18 +122,17 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
       (rows > 0 && (!coeffs || !coding)) || (ncopy > 0 && !copy_out))
     return set_error(NXEC_ERR_INVALID, "nxec_encode_host: invalid arguments");
   if (len == 0) return NXEC_OK;
-  nxec_ctx_t *ctx = nullptr;
-  int rc = default_ctx(&ctx);
+  DefaultLease lease;
+  int rc = default_ctx(lease);
   if (rc) return rc;
-  struct InFlight {
-    int n;
-    InFlight() : n(g_host_calls.fetch_add(1) + 1) {}
-    ~InFlight() { g_host_calls.fetch_sub(1); }
-  } inflight;
+  nxec_ctx_t *ctx = lease.ctx;
+  // calls in flight on this call's device (its PCIe link): few take the
+  // pipelined zero-copy form, many the per-piece DMA form
+  const int inflight = lease.device_inflight;
   // chunk buffers that are already pinned (the chunk arena, registered
   // receive pools): straight to the GPU, no staging memcpy
   if (ncopy == 0) {
-    rc = encode_host_pinned(ctx, len, k, rows, coeffs, data, coding, inflight.n);
+    rc = encode_host_pinned(ctx, len, k, rows, coeffs, data, coding, inflight);
     if (rc != kNotPinned) return rc;
   }
   const int64_t stride = (static_cast<int64_t>(len) + 15) / 16 * 16;  // keep chunks 16-B aligned in staging
@@ -148,7 +145,7 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   // pinned staging while the copy engine and the kernel work on piece p-1;
   // outputs come back per piece.  Staging layout [k inputs][rows outputs]
   // [ncopy pass-through outputs], each chunk at a 16-byte stride.
-  const int64_t piece = (len >= 2 * kHostPiece && inflight.n <= 2) ? kHostPiece : stride;
+  const int64_t piece = (len >= 2 * kHostPiece && inflight <= 2) ? kHostPiece : stride;
   const int npieces = static_cast<int>((len + piece - 1) / piece);
   while (static_cast<int>(slot->events.size()) < npieces) {
     hipEvent_t ev;
@@ -167,7 +164,7 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   // PCIe (no copy-engine round trip: 1 caller 25.8 -> 33.6 GiB/s).  Many
   // callers: H2D -> kernel -> D2H per piece, whose copy engines share the link
   // better (4 callers 69.8 vs 52.0 GiB/s zero copy; profiles/r01_dropin*.jsonl).
-  uint8_t *hv = inflight.n <= 2 ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
+  uint8_t *hv = inflight <= 2 ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
   for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
     const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
     host_parallel_for(k, [&](int j) { stage_copy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
@@ -207,7 +204,7 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
             if (copy_idx && copy_idx[j] == o - rows) to = copy_out[o - rows];
         }
         if (to) std::memcpy(to + off, slot->h + (k + o) * stride + off, static_cast<size_t>(pl));
-      });
+      }, HostLane::kOut);
     }
   } else {
     (void)hipStreamSynchronize(slot->stream);
@@ -352,10 +349,9 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
       if (rc == NXEC_OK) digest_gpu_observe(len, (digest_clock_ns() - t0) * 1e-6);
     }
   } observe{len, rc, t_call};
-  nxec_ctx_t *ctx = nullptr;
-  rc = default_ctx(&ctx);
-  if (rc) return rc;
-  if ((rc = ensure_device(ctx->device))) return rc;
+  DefaultLease lease;
+  if ((rc = default_ctx(lease))) return rc;
+  nxec_ctx_t *ctx = lease.ctx;
   DigestJob job;
   job.len = len;
   job.k = k;

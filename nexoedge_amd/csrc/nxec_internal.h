@@ -12,8 +12,10 @@
 namespace nxec {
 
 // Runs fn(i) for i in [0, n) on the library's host worker pool (staging
-// copies of the host entry points); returns when all are done.
-void host_parallel_for(int n, const std::function<void(int)> &fn);
+// copies of the host entry points); returns when all are done.  `lane`: the
+// copy's direction -- into pinned staging (kIn) or out of it (kOut).
+enum class HostLane { kIn, kOut };
+void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane = HostLane::kIn);
 
 // Digest placement of nxec_encode_host_md5 (nxec_digest_place.cpp): true if
 // the call's nhash digests of len bytes go to the host pool (their bytes are

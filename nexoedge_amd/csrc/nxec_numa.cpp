@@ -98,6 +98,26 @@ bool bind_thread_cpus(const std::vector<int> &cpus) {
   return n > 0 && pthread_setaffinity_np(pthread_self(), sizeof(want), &want) == 0;
 }
 
+// NUMA node of a CPU (-1: unknown), from the nodes' cpulists, read once
+int cpu_numa_node(int cpu) {
+  static const std::vector<int> node_of = [] {
+    std::vector<int> v;
+    std::string line;
+    std::vector<int> cpus;
+    for (int nd = 0; nd < 64; nd++) {
+      if (!read_line(sysfs_root() + "/sys/devices/system/node/node" + std::to_string(nd) + "/cpulist", &line) ||
+          !parse_cpulist(line, &cpus))
+        continue;
+      for (int c : cpus) {
+        if (static_cast<size_t>(c) >= v.size()) v.resize(c + 1, -1);
+        v[c] = nd;
+      }
+    }
+    return v;
+  }();
+  return cpu >= 0 && static_cast<size_t>(cpu) < node_of.size() ? node_of[cpu] : -1;
+}
+
 int device_bus_id(int device, char *buf, int len) {
   const hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
   if (e != hipSuccess) {

@@ -4,7 +4,9 @@
 // Proxy::writeFileStripes as one launch (proxy_file_ops.cc:557-666), and the
 // object layouts they follow (rs.cc:52-55, chunk_manager.cc:390-399).
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "nxec_runtime.h"
@@ -175,6 +177,9 @@ int nxec_encode_objects_ex(nxec_ctx_t *ctx, int n, int k, int nobjects, const un
   // chunks of a last stripe past the object's data read the context's zero line
   const uint8_t *zl = nullptr;
   if (fused && tail_total > 0 && (rc = zero_line(ctx, size_t(M) + 256, &zl))) return rc;
+  // testing (NXEC_TEST_FAULT=zero_stall): hold the line between planning and
+  // launch, while another caller grows the context's line
+  if (zl && test_fault("zero_stall")) std::this_thread::sleep_for(std::chrono::milliseconds(400));
   bool any_mask = false;
   int64_t g = 0, toff = 0, pad_blocks = 0;
   for (int o = 0; o < nobjects; o++) {

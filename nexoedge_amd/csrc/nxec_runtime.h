@@ -140,11 +140,16 @@ struct nxec_ctx {
   std::mutex zero_mu;
   uint8_t *zero = nullptr;
   size_t zero_bytes = 0;
+  std::vector<uint8_t *> zero_retired;  // outgrown lines, freed by nxec_ctx_destroy
 };
 
 namespace nxec {
 
 int ensure_device(int device);
+// NUMA placement helpers (nxec_numa.cpp)
+std::vector<int> pci_node_cpus(const char *bus_id, int *node);
+int device_bus_id(int device, char *buf, int len);
+int cpu_numa_node(int cpu);  // -1: unknown
 // A slot of at least `bytes` from the context's pool (best fit).  Slots an
 // asynchronous call handed back busy go only to callers that may wait for
 // them (may_wait: the asynchronous multi-file write, once the context holds
@@ -155,8 +160,24 @@ void release_slot(nxec_ctx_t *ctx, Slot *s);
 // slot_bytes), or a private one in `priv` while another call holds the
 // context's; the caller releases `priv` when it did not get the lock.
 int batch_stage(nxec_ctx_t *ctx, size_t slot_bytes, std::unique_lock<std::mutex> &lk, ObjStage &priv, ObjStage **out);
-// The per-device context of the entry points that take none (the drop-in).
-int default_ctx(nxec_ctx_t **out);
+// A default context leased for one call of an entry point that takes none
+// (the drop-in): a member of the default pool (nxec_context.cpp), its device
+// made current for the call; the destructor hands the member back and makes
+// the caller's own device current again.
+class DefaultLease {
+ public:
+  DefaultLease() = default;
+  DefaultLease(const DefaultLease &) = delete;
+  DefaultLease &operator=(const DefaultLease &) = delete;
+  ~DefaultLease();
+  nxec_ctx_t *ctx = nullptr;
+  int device_inflight = 1;  // calls in flight on ctx's device, this one included
+ private:
+  friend int default_ctx(DefaultLease &lease);
+  void *member_ = nullptr;
+  int saved_device_ = -1;
+};
+int default_ctx(DefaultLease &lease);
 inline hipStream_t pick_stream(nxec_ctx_t *ctx, void *stream) {
   return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
 }

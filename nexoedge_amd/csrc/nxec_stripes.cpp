@@ -404,14 +404,54 @@ int nxec_batch_layout(int n, int64_t len, int flags, int64_t *chunk_stride, int6
 
 namespace {
 std::mutex g_tuned_mu;
-std::map<std::tuple<int, int, int, int64_t, int>, std::pair<int64_t, int64_t>> g_tuned;
+// (device, n, k, len, flags, budget_bytes): a later caller asking for a
+// measurement at another budget gets its own (small scratch batches can rank
+// the candidates differently from full-size ones)
+std::map<std::tuple<int, int, int, int64_t, int, int64_t>, std::pair<int64_t, int64_t>> g_tuned;
 }  // namespace
+
+int nxec_layout_choose(int ncand, int rounds, const double *scores, double min_margin) {
+  if (ncand < 1 || rounds < 1 || !scores || min_margin < 0)
+    return set_error(NXEC_ERR_INVALID, "nxec_layout_choose: invalid arguments");
+  auto at = [&](int r, int c) { return scores[static_cast<size_t>(r) * ncand + c]; };
+  // relative spread of a candidate's scores across the rounds (-1: not measured in some round)
+  auto spread = [&](int c, double *mean) {
+    double lo = at(0, c), hi = lo, sum = 0;
+    for (int r = 0; r < rounds; r++) {
+      const double v = at(r, c);
+      if (!(v > 0)) return -1.0;
+      lo = std::min(lo, v);
+      hi = std::max(hi, v);
+      sum += v;
+    }
+    *mean = sum / rounds;
+    return (hi - lo) / *mean;
+  };
+  double inc_mean = 0;
+  const double inc_spread = spread(0, &inc_mean);
+  if (inc_spread < 0) return 0;  // the incumbent unmeasured: keep it
+  int best = 0;
+  double best_mean = inc_mean;
+  for (int c = 1; c < ncand; c++) {
+    double mean = 0;
+    const double sp = spread(c, &mean);
+    if (sp < 0) continue;
+    const double margin = std::max({min_margin, sp, inc_spread});
+    bool wins = true;
+    for (int r = 0; r < rounds && wins; r++) wins = at(r, c) > at(r, 0) * (1.0 + margin);
+    if (wins && mean > best_mean) {
+      best = c;
+      best_mean = mean;
+    }
+  }
+  return best;
+}
 
 int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flags, int64_t budget_bytes,
                             int64_t *chunk_stride, int64_t *stripe_stride) {
   if (!ctx || !valid_nk(n, k) || n == k || len <= 0 || !chunk_stride || !stripe_stride)
     return set_error(NXEC_ERR_INVALID, "nxec_batch_layout_tuned: invalid arguments");
-  const auto key = std::make_tuple(ctx->device, n, k, len, flags);
+  const auto key = std::make_tuple(ctx->device, n, k, len, flags, budget_bytes);
   {
     std::lock_guard<std::mutex> lk(g_tuned_mu);
     auto it = g_tuned.find(key);
@@ -460,10 +500,12 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
         std::find(scattered.begin(), scattered.end(), c) == scattered.end())
       scattered.push_back(c);
   std::sort(scattered.begin(), scattered.end());
-  // every candidate scored in two interleaved rounds (the device's state
-  // drifts less between candidates than between calls), scores summed
-  std::vector<double> score(cand.size(), 0.0);
-  for (int round = 0; round < 2 && !rc; round++) {
+  // every candidate scored in kRounds interleaved rounds (the device's state
+  // drifts less between candidates than between calls)
+  constexpr int kRounds = 3;
+  const int nc = static_cast<int>(cand.size());
+  std::vector<double> score(static_cast<size_t>(kRounds) * nc, 0.0);
+  for (int round = 0; round < kRounds && !rc; round++) {
     for (size_t ci = 0; ci < cand.size() && !rc; ci++) {
       const auto &c = cand[ci];
       const int64_t ns = budget / c.second;
@@ -491,18 +533,12 @@ int nxec_batch_layout_tuned(nxec_ctx_t *ctx, int n, int k, int64_t len, int flag
       if ((rc = rate_of(nullptr, &r_enc)) || (rc = rate_of(&first, &r_first)) || (rc = rate_of(&scattered, &r_scat)))
         break;
       const double w = (flags & NXEC_LAYOUT_RECOVER_HEAVY) ? 2.0 : 1.0;
-      score[ci] += (r_enc + r_first + w * r_scat) / (2.0 + w);
+      score[static_cast<size_t>(round) * nc + ci] = (r_enc + r_first + w * r_scat) / (2.0 + w);
     }
   }
-  // the table's layout (the first candidate) stays unless another scores 0.5 % higher
-  double best = -1;
-  std::pair<int64_t, int64_t> pick = {c0, s0};
-  for (size_t ci = 0; ci < cand.size(); ci++) {
-    if (score[ci] > 0 && (best < 0 || score[ci] > best * 1.005)) {
-      best = score[ci];
-      pick = cand[ci];
-    }
-  }
+  // the table's layout (the incumbent, candidate 0) stays unless another
+  // beats it in every round by more than the rounds' own spread (and 0.5 %)
+  const std::pair<int64_t, int64_t> pick = rc ? cand[0] : cand[nxec_layout_choose(nc, kRounds, score.data(), 0.005)];
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   (void)hipStreamSynchronize(st);

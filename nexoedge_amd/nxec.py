@@ -221,6 +221,43 @@ def device_info(dev: int = 0) -> dict:
     return {"arch": name.value.decode(), "cus": cus.value, "mem": mem.value}
 
 
+def default_devices(devices=None) -> None:
+    """nxec_default_devices: the default pool of the drop-in entry points.
+    None: one context per visible device (the default); "current": the
+    calling thread's current device; a list: those devices, one context per
+    entry (duplicates allowed)."""
+    if devices is None:
+        check(lib.nxec_default_devices(None, 0), "nxec_default_devices")
+    elif devices == "current":
+        check(lib.nxec_default_devices(None, -1), "nxec_default_devices")
+    else:
+        arr = (C.c_int * len(devices))(*[int(d) for d in devices])
+        check(lib.nxec_default_devices(arr, len(devices)), "nxec_default_devices")
+
+
+def default_pool_stats() -> list:
+    """[{device, node, calls, inflight}] per member of the default pool."""
+    cnt = C.c_int()
+    check(lib.nxec_default_pool_stats(None, None, None, None, 0, C.byref(cnt)), "nxec_default_pool_stats")
+    n = cnt.value
+    dv, nd, inf = (C.c_int * max(n, 1))(), (C.c_int * max(n, 1))(), (C.c_int * max(n, 1))()
+    calls = (C.c_ulonglong * max(n, 1))()
+    check(lib.nxec_default_pool_stats(dv, nd, calls, inf, n, C.byref(cnt)), "nxec_default_pool_stats")
+    return [{"device": dv[i], "node": nd[i], "calls": calls[i], "inflight": inf[i]} for i in range(min(n, cnt.value))]
+
+
+def default_pick(inflight: Sequence[int], nodes: Optional[Sequence[int]] = None, caller_node: int = -1,
+                 prev: int = -1) -> int:
+    """nxec_default_pick: the member the default pool leases for one call."""
+    n = len(inflight)
+    inf = (C.c_int * n)(*inflight)
+    nd = (C.c_int * n)(*nodes) if nodes is not None else None
+    r = lib.nxec_default_pick(n, inf, nd, int(caller_node), int(prev))
+    if r < 0:
+        check(r, "nxec_default_pick")
+    return r
+
+
 def set_device(dev: int) -> None:
     """nxec_set_device: make `dev` the calling thread's current device (its
     allocations, e.g. DeviceBuffer, land there)."""
@@ -658,6 +695,29 @@ class Group:
         check(lib.nxec_group_rs_recover_stripes(C.c_void_p(self.ptr), n, k, C.c_void_p(f.ctypes.data), len(f), ptrs,
                                                 chunk_stride, stripe_stride, length, C.c_void_p(ns.ctypes.data)),
               "nxec_group_rs_recover_stripes")
+
+    def rs_encode_async(self, n: int, k: int, stripes: Sequence[int], chunk_stride: int, stripe_stride: int,
+                        length: int, nstripes: Sequence[int]) -> None:
+        """nxec_group_rs_encode_stripes_async: queued on every member, returns at once (errors at wait())."""
+        ptrs = (C.c_void_p * len(stripes))(*[int(x) for x in stripes])
+        ns = np.ascontiguousarray(list(nstripes), dtype=np.int64)
+        check(lib.nxec_group_rs_encode_stripes_async(C.c_void_p(self.ptr), n, k, ptrs, chunk_stride, stripe_stride,
+                                                     length, C.c_void_p(ns.ctypes.data)),
+              "nxec_group_rs_encode_stripes_async")
+
+    def rs_recover_async(self, n: int, k: int, failed: Sequence[int], stripes: Sequence[int], chunk_stride: int,
+                         stripe_stride: int, length: int, nstripes: Sequence[int]) -> None:
+        f = np.ascontiguousarray(list(failed), dtype=np.int32)
+        ptrs = (C.c_void_p * len(stripes))(*[int(x) for x in stripes])
+        ns = np.ascontiguousarray(list(nstripes), dtype=np.int64)
+        check(lib.nxec_group_rs_recover_stripes_async(C.c_void_p(self.ptr), n, k, C.c_void_p(f.ctypes.data), len(f),
+                                                      ptrs, chunk_stride, stripe_stride, length,
+                                                      C.c_void_p(ns.ctypes.data)),
+              "nxec_group_rs_recover_stripes_async")
+
+    def wait(self) -> None:
+        """nxec_group_wait: every queued call done on every member (raises the first member failure)."""
+        check(lib.nxec_group_wait(C.c_void_p(self.ptr)), "nxec_group_wait")
 
     def close(self) -> None:
         if self.ptr:

@@ -300,7 +300,7 @@ def test_round5_entry_points_without_a_device():
 
 DEPLOYMENT_SETTINGS = {"NXEC_HOST_THREADS", "NXEC_HOST_DIRECT", "NXEC_SLOT_POOL_MAX", "NXEC_HOST_ARENA_MAX",
                        "NXEC_CHUNK_ARENA_MIN", "NXEC_CHUNK_MD5", "NXEC_DIGEST_PLACE", "NXEC_DIGEST_THREADS",
-                       "NXEC_DIGEST_CPUS"}
+                       "NXEC_DIGEST_CPUS", "NXEC_DEFAULT_DEVICES"}
 TEST_HOOKS = {"NXEC_TEST_FAULT", "NXEC_SYSFS_ROOT"}
 
 

@@ -971,12 +971,51 @@ def test_group_contexts_host_and_device(gpu_ctx, members):
         gpu_ctx.sync()
         g.rs_recover(n, k, [1, 4, 11, 13], [b.ptr for b in bufs], cs, n * cs, cs, counts)
         assert [b.checksum() for b in bufs] == sums
+        # the asynchronous forms: erase other chunks, queue a re-encode and two
+        # recovers on every member, one wait (bench.py --group's step)
+        for b, c in zip(bufs, counts):
+            erase_chunks(gpu_ctx, b, n, cs, c, [0, 2, 9, 12])
+        gpu_ctx.sync()
+        ptrs = [b.ptr for b in bufs]
+        g.rs_recover_async(n, k, [0, 2, 9, 12], ptrs, cs, n * cs, cs, counts)
+        g.rs_encode_async(n, k, ptrs, cs, n * cs, cs, counts)
+        g.rs_recover_async(n, k, [3, 5, 6, 10], ptrs, cs, n * cs, cs, counts)
+        g.wait()
+        assert [b.checksum() for b in bufs] == sums
         for i, b in enumerate(bufs):
             got = b.download().reshape(counts[i], n, cs)
             for s in range(counts[i]):
                 want = oracle.matmul(enc, list(data[starts[i] + s].reshape(k, cs)))
                 assert np.array_equal(got[s, :k], data[starts[i] + s].reshape(k, cs)), (i, s)
                 assert all(np.array_equal(got[s, k + r], want[r]) for r in range(p)), (i, s)
+        for b in bufs:
+            b.free()
+    finally:
+        g.close()
+
+
+def test_group_async_member_failure_surfaces_from_wait(gpu_ctx):
+    """A member whose shard is invalid (a negative stripe count) fails inside
+    its own thread; the asynchronous call has already returned, so the failure
+    is kept and the next nxec_group_wait raises it, naming the device.  The
+    other members' work still ran, and the wait after that one is clean."""
+    n, k, cs, members = 14, 10, 4096, 3
+    g = nxec.Group([0] * members)
+    try:
+        data = [fill_bytes(k * cs, 7700 + s) for s in range(members)]
+        bufs = [stripe_buffer(n, k, cs, cs, [d])[0] for d in data]
+        ptrs = [b.ptr for b in bufs]
+        g.rs_encode_async(n, k, ptrs, cs, n * cs, cs, [1, -1, 1])
+        with pytest.raises(nxec.NxecError) as ei:
+            g.wait()
+        assert "device 0" in str(ei.value)
+        enc = nxec.gen_rs_matrix(n, k)[k:]
+        for i in (0, 2):  # the valid members encoded their stripe
+            got = bufs[i].download().reshape(n, cs)
+            want = oracle.matmul(enc, list(data[i].reshape(k, cs)))
+            assert all(np.array_equal(got[k + r], want[r]) for r in range(n - k)), i
+        g.rs_encode_async(n, k, ptrs, cs, n * cs, cs, [1, 1, 1])
+        g.wait()
         for b in bufs:
             b.free()
     finally:
