@@ -15,7 +15,8 @@ OBJDIR   := build/obj
 
 LIB_SRCS := $(CSRC)/gf_host.cpp $(CSRC)/nxec_context.cpp $(CSRC)/nxec_stripes.cpp $(CSRC)/nxec_objects.cpp \
             $(CSRC)/nxec_host_paths.cpp $(CSRC)/nxec_host_encode.cpp $(CSRC)/nxec_agent.cpp $(CSRC)/nxec_probes.cpp \
-            $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip $(CSRC)/nxec_files_md5.hip \
+            $(CSRC)/nxec_kernels.hip $(CSRC)/nxec_md5.hip $(CSRC)/nxec_encode_md5.hip $(CSRC)/nxec_encode_md5_ring.hip \
+            $(CSRC)/nxec_files_md5.hip \
             $(CSRC)/nxec_group.cpp $(CSRC)/nxec_host_arena.cpp $(CSRC)/nxec_digest.cpp $(CSRC)/nxec_digest_place.cpp $(CSRC)/nxec_numa.cpp $(CSRC)/nxec_config.cpp \
             $(CSRC)/coding/rs.cc $(CSRC)/coding/coding_options.cc $(CSRC)/coding/stripe_batch.cc
 LIB_OBJS := $(patsubst $(CSRC)/%,$(OBJDIR)/%.o,$(LIB_SRCS))

@@ -225,6 +225,11 @@ void ObjStage::release() {
     streams[i] = nullptr;
     h2d_done[i] = nullptr;
   }
+  if (aux) {
+    (void)hipStreamSynchronize(aux);
+    (void)hipStreamDestroy(aux);
+    aux = nullptr;
+  }
   if (d) (void)hipFree(d);
   d = nullptr;
   cap = 0;

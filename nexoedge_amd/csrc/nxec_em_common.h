@@ -303,6 +303,139 @@ __device__ __forceinline__ void hash_rows_hg(const uint8_t *buf, uint32_t buf_by
 }
 
 
+// ---- the decoupled form (k_mul_md5_ring) ----
+// A ring of kRingSlots LDS buffers of kRingStep bytes per hashed chunk,
+// handed between the roles by per-slot counters in LDS instead of a
+// workgroup barrier per step: the code waves fill a slot once the hash waves
+// have counted it free, the hash waves read it once the code waves have
+// counted it ready.  Each role then waits only when the other is a whole
+// ring behind or ahead, so a slow step of one role no longer stalls the other
+// (a barrier per step cost every step the slower role's time).
+constexpr int kRingStep = 128;               // bytes of a chunk per hash step (2 MD5 blocks)
+constexpr int kRingRow = kRingStep + 16;     // row stride: a quarter-wave's 16-byte reads on distinct banks
+constexpr int kRingSlots = 4;                // two code steps (256 bytes each) of slack
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32m;
+__device__ __forceinline__ lds_u32m *lds_word(uint32_t byte_off) {
+  return reinterpret_cast<lds_u32m *>(static_cast<uintptr_t>(byte_off));
+}
+// The wave waits (s_sleep between polls) until the LDS counter at byte
+// cnt_off reaches `need`.  One asm block, not a C++ loop: a loop in the code
+// waves' unrolled step would be a CFG loop inside the load ring, where the
+// waitcnt pass drains every outstanding load at the loop head and register
+// allocation splits the ring's live ranges (256 VGPRs + spills at k = 10).
+// The poll's own s_waitcnt lgkmcnt(0) also orders the LDS reads that follow.
+__device__ __forceinline__ void ring_wait(uint32_t cnt_off, uint32_t need) {
+  uint32_t v, sv;
+  asm volatile(
+      "nxec_ring_poll_%=:\n"
+      "  ds_read_b32 %0, %2\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  v_readfirstlane_b32 %1, %0\n"
+      "  s_cmp_ge_u32 %1, %3\n"
+      "  s_cbranch_scc1 nxec_ring_done_%=\n"
+      "  s_sleep 1\n"
+      "  s_branch nxec_ring_poll_%=\n"
+      "nxec_ring_done_%=:"
+      : "=&v"(v), "=&s"(sv)
+      : "v"(cnt_off), "s"(need)
+      : "scc", "memory");
+}
+// The counter at byte off, read now and waited for at its first use: issued a
+// step early, its value is there when ring_wait_from looks at it, so a role
+// that is not behind pays no LDS round trip per step.
+__device__ __forceinline__ uint32_t ring_peek(uint32_t off) {
+  return __hip_atomic_load(lds_word(off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// ring_wait with an earlier read of the counter: returns at once when `seen`
+// already reaches `need`, else polls (one asm block, as ring_wait).
+// MEM: a compiler memory barrier too (the code waves: no LDS write of the
+// slot may move above the wait); the hash waves order their reads with
+// sched_barrier instead, so the waitcnt pass keeps their reads in flight.
+template <bool MEM = true>
+__device__ __forceinline__ void ring_wait_from(uint32_t seen, uint32_t cnt_off, uint32_t need) {
+  uint32_t v, sv;
+  if (MEM)
+  asm volatile(
+      "  v_readfirstlane_b32 %1, %4\n"
+      "  s_cmp_ge_u32 %1, %3\n"
+      "  s_cbranch_scc1 nxec_ringf_done_%=\n"
+      "nxec_ringf_poll_%=:\n"
+      "  s_sleep 1\n"
+      "  ds_read_b32 %0, %2\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  v_readfirstlane_b32 %1, %0\n"
+      "  s_cmp_ge_u32 %1, %3\n"
+      "  s_cbranch_scc0 nxec_ringf_poll_%=\n"
+      "nxec_ringf_done_%=:"
+      : "=&v"(v), "=&s"(sv)
+      : "v"(cnt_off), "s"(need), "v"(seen)
+      : "scc", "memory");
+  else
+  asm volatile(
+      "  v_readfirstlane_b32 %1, %4\n"
+      "  s_cmp_ge_u32 %1, %3\n"
+      "  s_cbranch_scc1 nxec_ringh_done_%=\n"
+      "nxec_ringh_poll_%=:\n"
+      "  s_sleep 1\n"
+      "  ds_read_b32 %0, %2\n"
+      "  s_waitcnt lgkmcnt(0)\n"
+      "  v_readfirstlane_b32 %1, %0\n"
+      "  s_cmp_ge_u32 %1, %3\n"
+      "  s_cbranch_scc0 nxec_ringh_poll_%=\n"
+      "nxec_ringh_done_%=:"
+      : "=&v"(v), "=&s"(sv)
+      : "v"(cnt_off), "s"(need), "v"(seen)
+      : "scc");
+}
+// ring_signal once all but the wave's last 9 LDS operations are complete
+// (LDS operations complete in order; scalar loads in lgkmcnt only make the
+// wait longer).  The hash waves' form: no compiler memory barrier (their
+// reads are ordered by sched_barrier), so the waitcnt pass keeps the reads
+// issued before it in flight.
+__device__ __forceinline__ void ring_signal_behind9(uint32_t cnt_off) {
+  uint64_t save;
+  const uint32_t one = 1;
+  asm volatile(
+      "s_waitcnt lgkmcnt(9)\n"
+      "  s_mov_b64 %0, exec\n"
+      "  s_mov_b64 exec, 1\n"
+      "  ds_add_u32 %1, %2\n"
+      "  s_mov_b64 exec, %0"
+      : "=&s"(save)
+      : "v"(cnt_off), "v"(one));
+}
+// Once the wave's LDS accesses so far are complete, lane 0 alone adds 1 to the
+// counter at byte cnt_off (and at cnt_off2 when it differs).  Also one asm
+// block: a lane-0 branch would be divergent control flow inside the code
+// waves' unrolled step.
+__device__ __forceinline__ void ring_signal(uint32_t cnt_off, uint32_t cnt_off2 = 0xffffffffu) {
+  uint64_t save;
+  const uint32_t one = 1;
+  if (cnt_off2 == 0xffffffffu) {
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n"
+        "  s_mov_b64 %0, exec\n"
+        "  s_mov_b64 exec, 1\n"
+        "  ds_add_u32 %1, %2\n"
+        "  s_mov_b64 exec, %0"
+        : "=&s"(save)
+        : "v"(cnt_off), "v"(one)
+        : "memory");
+  } else {
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n"
+        "  s_mov_b64 %0, exec\n"
+        "  s_mov_b64 exec, 1\n"
+        "  ds_add_u32 %1, %3\n"
+        "  ds_add_u32 %2, %3\n"
+        "  s_mov_b64 exec, %0"
+        : "=&s"(save)
+        : "v"(cnt_off), "v"(cnt_off2), "v"(one)
+        : "memory");
+  }
+}
+
 // ring depth of the pointer-table form: as many steps in flight as ~200
 // VGPRs hold (its 64-bit source pointers take 2K of them), at most 8 -- its
 // loads cross PCIe (microseconds each), so small k keeps more steps ahead
@@ -312,5 +445,9 @@ constexpr int gm_depth() {
 }
 
 }  // namespace
+
+// k_mul_md5_ring (nxec_encode_md5_ring.hip) for (hash_src, k), and its kernel attributes
+void (*mul_md5_ring_kernel(bool hash_src, int k))(const MulMd5Args);
+int prepare_encode_md5_ring();
 
 }  // namespace nxec

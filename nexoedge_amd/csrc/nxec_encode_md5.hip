@@ -432,6 +432,9 @@ bool mul_md5_eligible(int k, int rows, int64_t len, const void *src, int64_t src
 }
 
 int prepare_encode_md5() {
+#if NXEC_DESIGN_PROBES
+  if (int rc = prepare_encode_md5_ring()) return rc;
+#endif
   for (int i = 0; i < 2 * kEncMd5MaxK; i++) {
     const EmKernel fn = kEm[i / kEncMd5MaxK][i % kEncMd5MaxK];
     hipFuncAttributes fa{};
@@ -491,6 +494,15 @@ int launch_mul_md5(const MulMd5Args &in, int num_cus, void *stream) {
   if (grid >= (int64_t(1) << 31)) return set_error(NXEC_ERR_INVALID, "encode+md5: batch too large for one launch");
   int lds = a.k * 1024 + static_cast<int>(2 * S * n * kEmRow);
   EmKernel fn = kEm[a.hash_src ? 1 : 0][a.k - 1];
+#if NXEC_DESIGN_PROBES
+  // A/B: the decoupled form where its ring fits the LDS (k <= 20, S * n <=
+  // 256 rows of 4 x 144 bytes: all but the widest hashed-source stripes)
+  const int lds_ring = a.k * 1024 + static_cast<int>(kRingSlots * S * n * kRingRow) + 8 * 4;
+  if (tuning().em_ring && lds_ring <= kEmLds) {
+    fn = mul_md5_ring_kernel(a.hash_src != 0, a.k);
+    lds = lds_ring;
+  }
+#endif
 #if NXEC_DESIGN_PROBES
   if (tuning().em_probe >= 0 && a.k == 10 && a.hash_src) fn = kEmProbe[tuning().em_probe & 7];
   // A/B: conflict-free split-nibble tables (k = 10, sources hashed; 40 KiB of tables)

@@ -439,8 +439,16 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
   ObjStage priv, *pstg = nullptr;
   if ((rc = batch_stage(ctx, size_t(B) * 2 * k * stride, lk, priv, &pstg))) return rc;
   ObjStage &stg = *pstg;
-  // batch b lives in staging slot b % kObjSlots; one stream per stage
-  hipStream_t s_gather = stg.streams[0], s_decode = stg.streams[1], s_scatter = stg.streams[2];
+  // batch b lives in staging slot b % kObjSlots; one stream per stage, none
+  // of them the context's own (the gather's per-piece syncs on a
+  // borrowed context stream waited for other callers' work)
+  if (stg.borrowed0 && !stg.aux &&
+      (rc = hip_check(hipStreamCreateWithFlags(&stg.aux, hipStreamNonBlocking), "decode_frames gather stream"))) {
+    if (!lk.owns_lock()) priv.release();
+    return rc;
+  }
+  hipStream_t s_gather = stg.borrowed0 ? stg.aux : stg.streams[0], s_decode = stg.streams[1],
+              s_scatter = stg.streams[2];
   std::mutex mu;
   std::condition_variable cv;
   int64_t gathered = 0, decoded = 0, scattered = 0;  // batches done per stage
@@ -516,7 +524,8 @@ int nxec_decode_frames(nxec_ctx_t *ctx, int n, int k, const int32_t *failed, int
   }
   if (gatherer.joinable()) gatherer.join();
   if (scatterer.joinable()) scatterer.join();
-  for (int i = 0; i < kObjSlots; i++) (void)hipStreamSynchronize(stg.streams[i]);
+  (void)hipStreamSynchronize(s_gather);
+  for (int i = 1; i < kObjSlots; i++) (void)hipStreamSynchronize(stg.streams[i]);
   if (!lk.owns_lock()) priv.release();
   if (err) restore_error(err_msg);
   return err;

@@ -22,6 +22,7 @@ Tuning read_tuning() {
   if ((e = knob("NXEC_FUSED_MD5"))) t.fused_md5 = e[0] != '0';
   if ((e = knob("NXEC_EM_S"))) t.em_stripes = std::atoi(e);
   if ((e = knob("NXEC_EM_PRIO"))) t.em_prio = std::atoi(e);
+  if ((e = knob("NXEC_EM_RING"))) t.em_ring = e[0] == '1';
   if ((e = knob("NXEC_EM_PROBE"))) t.em_probe = std::atoi(e);
   if ((e = knob("NXEC_EM_TABLES"))) t.em_nibble = e[0] == 'n';
   if ((e = knob("NXEC_EM_HASHSRC"))) t.em_hashsrc_global = e[0] == 'g';

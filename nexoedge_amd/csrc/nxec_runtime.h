@@ -94,6 +94,10 @@ struct ObjStage {
   hipStream_t streams[kObjSlots] = {};
   hipEvent_t h2d_done[kObjSlots] = {};
   bool borrowed0 = false;  // streams[0] is the context's stream
+  // nxec_decode_frames' gather stream when streams[0] is borrowed (a gather
+  // synchronises its stream per piece: on the context's stream that would
+  // wait for other threads' work queued there too); made on first use
+  hipStream_t aux = nullptr;
   void release();
 };
 

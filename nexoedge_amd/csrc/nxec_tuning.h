@@ -21,6 +21,7 @@ struct Tuning {
   bool fused_md5 = true;      // NXEC_FUSED_MD5=0: coding and MD5 as separate launches
   int em_stripes = 0;         // NXEC_EM_S: stripes per k_mul_md5 workgroup (0 = by batch)
   int em_prio = 0;            // NXEC_EM_PRIO: s_setprio of the hash waves
+  bool em_ring = false;       // NXEC_EM_RING=1: k_mul_md5_ring, the roles decoupled by LDS counters
   int em_probe = -1;          // NXEC_EM_PROBE: k_mul_md5 role probe (outputs invalid)
   bool em_nibble = false;     // NXEC_EM_TABLES=nib: split-nibble tables
   bool em_hashsrc_global = false;  // NXEC_EM_HASHSRC=global: hash lanes read sources from L2

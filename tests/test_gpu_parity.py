@@ -1217,6 +1217,32 @@ def test_decode_frames_pipelined(gpu_ctx, failed, batch):
         gpu_ctx.decode_frames(n, k, failed, bad, [o.ctypes.data for o in outs], cs, ns, batch)
 
 
+def test_decode_frames_pinned_large_frames(gpu_ctx):
+    """nxec_decode_frames with pinned frames of >= 8 MiB (the
+    gather and scatter then DMA each frame directly, kFrameDirect) -- every
+    data chunk lands in its pinned output frame, equal to the original; two
+    batches, so the pipeline's gather, decode and scatter overlap."""
+    n, k, cs, ns = 6, 4, (8 << 20) + 48, 3
+    failed = [0, 5]
+    enc = nxec.gen_rs_matrix(n, k)
+    data = [fill_bytes(k * cs, 8700 + s).reshape(k, cs) for s in range(ns)]
+    chunks = [np.concatenate([d, np.stack(oracle.matmul(enc[k:], list(d)))]) for d in data]
+    pin_in = nxec.PinnedBuffer(ns * n * cs)
+    pin_out = nxec.PinnedBuffer(ns * k * cs)
+    try:
+        pin_in.array[:] = np.concatenate([c.reshape(-1) for c in chunks])
+        pin_out.array[:] = 0xEE
+        in_frames = [0 if c in failed else pin_in.ptr + (s * n + c) * cs for s in range(ns) for c in range(n)]
+        out_frames = [pin_out.ptr + i * cs for i in range(ns * k)]
+        gpu_ctx.decode_frames(n, k, failed, in_frames, out_frames, cs, ns, 2)
+        got = pin_out.array.reshape(ns, k, cs)
+        for s in range(ns):
+            assert np.array_equal(got[s], data[s]), s
+    finally:
+        pin_in.free()
+        pin_out.free()
+
+
 @pytest.mark.parametrize("mode", ["pinned", "registered", "pageable"])
 def test_rs_recover_frames(gpu_ctx, mode):
     """Recover the failed chunks straight into their host frames: zero copy for
