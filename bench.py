@@ -220,7 +220,7 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    # round-5 passes on the shipped library (tools/gpu_r05_final.sh; every dispatch
+    # round-5 passes on the shipped library (tools/archive/gpu_r05_final.sh; every dispatch
     # of the roofline kernel labelled with the bench line's bytes per launch);
     # tests/test_bench_line.py checks each file's labels and reports its lib_sha16
     # against libnxec.so; only the default layout the passes ran with (other
