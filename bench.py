@@ -763,7 +763,7 @@ def group_measure(args):
     ranks), each step the headline's encode + recover (rotating patterns)
     through nxec_group_rs_{encode,recover}_stripes_async -- each member's
     long-lived thread queues both launches on its stream, one nxec_group_wait
-    per step (the ranks' pattern).  Verified as the ranks' run: the
+    after the timed steps (the ranks' pattern: queue every step, sync once).  Verified as the ranks' run: the
     batches' checksums survive the timed steps, and erased chunks of every
     member come back.  Aggregate user-visible GiB/s of all members."""
     n, k, cs, ns = args.n, args.k, args.chunk, args.stripes
@@ -789,17 +789,18 @@ def group_measure(args):
             out.append(b.checksum())
         return out
 
-    def step(i):  # queued on every member's thread and stream; one wait per step, as the ranks
+    def step(i):  # queued on every member's thread and stream; as the ranks, one wait after the steps
         g.rs_encode_async(n, k, ptrs, cst, stripe, cs, counts)
         g.rs_recover_async(n, k, PATTERNS[i % len(PATTERNS)], ptrs, cst, stripe, cs, counts)
-        g.wait()
 
     for i in range(max(1, args.warmup)):
         step(i)
+    g.wait()
     want = sums()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+    g.wait()
     dt = time.perf_counter() - t0
     verified = sums() == want
     # erase the third pattern's chunks in every member's batch for real, rebuild them
@@ -820,7 +821,7 @@ def group_measure(args):
             "devices": devices, "stripes_per_member": ns, "steps": args.steps, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "verified": verified, "layout": lay,
             "note": "one process, nxec_group: a long-lived host thread + context per member, encode + recover "
-                    "queued per step, one group wait; "
+                    "queued every step, one group wait after the steps (as the ranks sync once); "
                     "encode (k+p)*cs + recover (k+e)*cs per stripe as the headline"}
 
 

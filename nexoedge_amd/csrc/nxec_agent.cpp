@@ -81,7 +81,7 @@ int agent_finish(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int64_t cs, AgentB
     const uint8_t *dg = b.slot->h + b.md5_off + i * size_t(nh) * 16;
     if (o == 0 && r.md5) std::memcpy(r.md5, dg + size_t(b.hsrc) * 16, size_t(no) * 16);
     if (o == 0 && r.md5_inputs && b.hsrc) std::memcpy(r.md5_inputs, dg, size_t(b.hsrc) * 16);
-  }, HostLane::kOut);
+  }, HostLane::kOut, ctx->numa_node);
   b.reqs.clear();
   return NXEC_OK;
 }
@@ -140,7 +140,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
       unsigned char *p = reqs[ids[o / no]].outputs[o % no];
       out_dv[o] = aligned16(p) ? reinterpret_cast<uintptr_t>(host_device_view_range(p, cs)) : 0;
     }
-  });
+  }, HostLane::kIn, ctx->numa_node);
   if (agent_trace())
     std::fprintf(stderr, "agent fused group of %zu: classify %zu buffers %.3f ms\n", nid, nid * (ni + no),
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count());
@@ -202,7 +202,7 @@ static int agent_fused_group(nxec_ctx_t *ctx, const nxec_agent_req *reqs, const 
         const size_t o = q - nb * ni;
         dst_tab[o] = b.out_pos[o] < 0 ? out_dv[first * no + o] : reinterpret_cast<uintptr_t>(hv + b.out_pos[o]);
       }
-    });
+    }, HostLane::kIn, ctx->numa_node);
     for (size_t i = first; i < last; i++) b.reqs.push_back(ids[i]);
     if (agent_trace()) {
       const auto tr2 = std::chrono::steady_clock::now();
@@ -303,7 +303,7 @@ static int agent_encode_impl(nxec_ctx_t *ctx, const nxec_agent_req *reqs, int nr
         const int64_t i = item / ni;
         const int j = item % ni;
         stage_copy(b.slot->h + (i * ni + j) * stride, reqs[ids[first + i]].inputs[j], chunk_size);
-      });
+      }, HostLane::kIn, ctx->numa_node);
       for (int64_t i = 0; i < nb; i++) b.reqs.push_back(ids[first + i]);
       if (agent_trace()) {
         const auto tr2 = std::chrono::steady_clock::now();

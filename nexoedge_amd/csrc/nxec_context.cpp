@@ -12,6 +12,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -73,13 +74,20 @@ class HostPool {
   // staging and copies out of it have a worker set each, so a pipelined
   // caller's gather and scatter (nxec_decode_frames) do not queue behind each
   // other's helper tasks; otherwise one shared pool (rounds 1-5).
-  static HostPool &get(HostLane lane) {
-    static HostPool in;
-    if (lane == HostLane::kOut && tuning().host_lanes) {
-      static HostPool out;
-      return out;
-    }
-    return in;
+  // One pool per NUMA node of the GPUs served (round 6): its threads run on
+  // that node's CPUs, next to the GPU's PCIe root and, by first touch, the
+  // staging they fill, instead of wherever the scheduler puts them (the
+  // pageable-frames read pipeline: 33 -> 39 GiB/s with its threads on the
+  // GPU's node, profiles/r06_frames_ab.jsonl).  Pools are made on first use
+  // and live for the process.
+  static HostPool &get(HostLane lane, int node) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, HostPool *> pools;
+    const int l = lane == HostLane::kOut && tuning().host_lanes ? 1 : 0;
+    std::lock_guard<std::mutex> lk(mu);
+    HostPool *&p = pools[{node, l}];
+    if (!p) p = new HostPool(node);
+    return *p;
   }
   // runs fn(i) for i in [0, n), returns when all are done.  The pool serves
   // two jobs at a time (a pipelined caller's gather and scatter,
@@ -122,10 +130,15 @@ class HostPool {
   }
 
  private:
-  HostPool() {
+  explicit HostPool(int node) {
     int nt = 8;  // deployment setting NXEC_HOST_THREADS
     if (const char *e = std::getenv("NXEC_HOST_THREADS")) nt = std::max(0, std::atoi(e));
-    for (int i = 0; i < nt; i++) workers_.emplace_back([this] { loop(); });
+    const std::vector<int> cpus = node_cpus(node);
+    for (int i = 0; i < nt; i++)
+      workers_.emplace_back([this, cpus] {
+        (void)bind_thread_cpus(cpus);  // within the process's affinity; unknown node: unbound
+        loop();
+      });
   }
   ~HostPool() {
     {
@@ -196,8 +209,12 @@ void *host_device_view_range(const void *h, size_t bytes) {
   return d0;
 }
 
-void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane) {
-  HostPool::get(lane).parallel_for(n, fn);
+void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane, int node) {
+  if (n <= 1) {  // nothing to spread: no pool (and no thread) needed
+    if (n == 1) fn(0);
+    return;
+  }
+  HostPool::get(lane, node).parallel_for(n, fn);
 }
 
 int set_error(int code, const char *fmt, ...) {
@@ -620,6 +637,10 @@ int nxec_ctx_create(int device, nxec_ctx_t **out) {
   hipDeviceProp_t prop;
   NXEC_HIP(hipGetDeviceProperties(&prop, device));
   ctx->num_cus = prop.multiProcessorCount;
+  {
+    char bus[64] = {0};
+    if (device_bus_id(device, bus, sizeof(bus)) == NXEC_OK) (void)pci_node_cpus(bus, &ctx->numa_node);
+  }
   NXEC_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
   *out = ctx.release();
   return NXEC_OK;

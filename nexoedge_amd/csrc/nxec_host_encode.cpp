@@ -104,7 +104,7 @@ int encode_host_pinned(nxec_ctx_t *ctx, int len, int k, int rows, const unsigned
         rows, [&](int r) {
           if (!out_mapped[r]) std::memcpy(coding[r], slot->h + chunk_off(k + r), size_t(len));
         },
-        HostLane::kOut);
+        HostLane::kOut, ctx->numa_node);
   release_slot(ctx, slot);
   return rc;
 }
@@ -167,7 +167,9 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
   uint8_t *hv = inflight <= 2 ? static_cast<uint8_t *>(host_device_view(slot->h)) : nullptr;
   for (int pc = 0; pc < npieces && rc == NXEC_OK; pc++) {
     const int64_t off = pc * piece, pl = std::min<int64_t>(piece, len - off);
-    host_parallel_for(k, [&](int j) { stage_copy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); });
+    host_parallel_for(
+        k, [&](int j) { stage_copy(slot->h + j * stride + off, data[j] + off, static_cast<size_t>(pl)); }, HostLane::kIn,
+        ctx->numa_node);
     hipError_t e = hipSuccess;
     uint8_t *base = hv ? hv : slot->d;
     if (!hv) {
@@ -204,7 +206,7 @@ int nxec_encode_host_ex(int len, int k, int rows, const unsigned char *coeffs, c
             if (copy_idx && copy_idx[j] == o - rows) to = copy_out[o - rows];
         }
         if (to) std::memcpy(to + off, slot->h + (k + o) * stride + off, static_cast<size_t>(pl));
-      }, HostLane::kOut);
+      }, HostLane::kOut, ctx->numa_node);
     }
   } else {
     (void)hipStreamSynchronize(slot->stream);

@@ -115,7 +115,7 @@ struct FramePlan {
 
 // host memcpy of items [first, first+count) between frames and staging, in
 // jobs of at most 1 MiB spread over the host pool
-void frame_copies(const FramePlan &fp, int64_t first, int64_t count, uint8_t *staging, HostLane lane,
+void frame_copies(const FramePlan &fp, int64_t first, int64_t count, uint8_t *staging, HostLane lane, int node,
                   const std::function<void(int64_t item, int64_t off, int64_t n, uint8_t *stage)> &copy) {
   const int64_t job = int64_t(1) << 20;
   const int64_t jobs_per_item = (fp.seg + job - 1) / job;
@@ -123,7 +123,7 @@ void frame_copies(const FramePlan &fp, int64_t first, int64_t count, uint8_t *st
     const int64_t i = t / jobs_per_item, o = (t % jobs_per_item) * job;
     const int64_t b = fp.bytes(first + i);
     if (o < b) copy(first + i, o, std::min(job, b - o), staging + i * fp.seg + o);
-  }, lane);
+  }, lane, node);
 }
 
 // whether every frame is pinned / registered host memory over its whole
@@ -169,7 +169,7 @@ int nxec_gather_chunks(nxec_ctx_t *ctx, const unsigned char *const *h_chunks, in
     const int s = static_cast<int>(p & 1);
     const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
     if (p >= 2 && (rc = hip_check(hipEventSynchronize(done[s]), "gather piece sync"))) break;
-    frame_copies(fp, first, count, slots[s]->h, HostLane::kIn, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
+    frame_copies(fp, first, count, slots[s]->h, HostLane::kIn, ctx->numa_node, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
       stage_copy(stage, h_chunks[fp.chunk(item)] + fp.off(item) + o, size_t(nb));
     });
     hipError_t e = hipSuccess;
@@ -235,7 +235,7 @@ int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src
     if (p + 1 < fp.npieces && (rc = issue(p + 1))) break;
     if ((rc = hip_check(hipEventSynchronize(done[s]), "scatter piece sync"))) break;
     const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
-    frame_copies(fp, first, count, slots[s]->h, HostLane::kOut, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
+    frame_copies(fp, first, count, slots[s]->h, HostLane::kOut, ctx->numa_node, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
       std::memcpy(h_chunks[fp.chunk(item)] + fp.off(item) + o, stage, size_t(nb));
     });
   }

@@ -13,9 +13,11 @@ namespace nxec {
 
 // Runs fn(i) for i in [0, n) on the library's host worker pool (staging
 // copies of the host entry points); returns when all are done.  `lane`: the
-// copy's direction -- into pinned staging (kIn) or out of it (kOut).
+// copy's direction -- into pinned staging (kIn) or out of it (kOut); `node`:
+// the NUMA node of the GPU the copies feed (its pool's threads run on that
+// node's CPUs; -1: unknown, an unbound pool).
 enum class HostLane { kIn, kOut };
-void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane = HostLane::kIn);
+void host_parallel_for(int n, const std::function<void(int)> &fn, HostLane lane = HostLane::kIn, int node = -1);
 
 // Digest placement of nxec_encode_host_md5 (nxec_digest_place.cpp): true if
 // the call's nhash digests of len bytes go to the host pool (their bytes are

@@ -98,6 +98,16 @@ bool bind_thread_cpus(const std::vector<int> &cpus) {
   return n > 0 && pthread_setaffinity_np(pthread_self(), sizeof(want), &want) == 0;
 }
 
+// CPUs of NUMA node `node` (empty: unknown)
+std::vector<int> node_cpus(int node) {
+  std::vector<int> cpus;
+  std::string line;
+  if (node < 0 || !read_line(sysfs_root() + "/sys/devices/system/node/node" + std::to_string(node) + "/cpulist", &line) ||
+      !parse_cpulist(line, &cpus))
+    cpus.clear();
+  return cpus;
+}
+
 // NUMA node of a CPU (-1: unknown), from the nodes' cpulists, read once
 int cpu_numa_node(int cpu) {
   static const std::vector<int> node_of = [] {

@@ -114,6 +114,7 @@ struct DigestJob;
 struct nxec_ctx {
   int device = 0;
   int num_cus = 0;
+  int numa_node = -1;  // of the device's PCIe root (-1: unknown): its host copies run on that node's pool
   hipStream_t stream = nullptr;
   std::mutex slot_mu;
   std::vector<nxec::Slot *> free_slots;
@@ -154,6 +155,8 @@ int ensure_device(int device);
 std::vector<int> pci_node_cpus(const char *bus_id, int *node);
 int device_bus_id(int device, char *buf, int len);
 int cpu_numa_node(int cpu);  // -1: unknown
+std::vector<int> node_cpus(int node);  // empty: unknown
+bool bind_thread_cpus(const std::vector<int> &cpus);
 // A slot of at least `bytes` from the context's pool (best fit).  Slots an
 // asynchronous call handed back busy go only to callers that may wait for
 // them (may_wait: the asynchronous multi-file write, once the context holds
