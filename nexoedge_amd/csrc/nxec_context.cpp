@@ -62,6 +62,34 @@ void stage_copy(void *dst, const void *src, size_t n) {
   std::memcpy(d + i, sp + i, n - i);
 }
 
+// Copy out of pinned staging into a caller's buffer.  With the NT-staging
+// probe the caller's lines are written with streaming stores too (no
+// read-for-ownership of a destination the CPU does not read next): the
+// read pipeline's host DRAM traffic per byte drops from ~4 to ~3 passes.
+void unstage_copy(void *dst, const void *src, size_t n) {
+  uint8_t *d = static_cast<uint8_t *>(dst);
+  const uint8_t *sp = static_cast<const uint8_t *>(src);
+  if (!tuning().nt_staging || n < 4096) {
+    std::memcpy(d, sp, n);
+    return;
+  }
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(d) & 15)) & 15;
+  std::memcpy(d, sp, head);
+  size_t i = head;
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 32));
+    const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i *>(sp + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i *>(d + i + 48), e);
+  }
+  _mm_sfence();
+  std::memcpy(d + i, sp + i, n - i);
+}
+
 namespace {
 
 // Host worker pool for staging copies (pageable <-> pinned) of the host entry

@@ -236,7 +236,7 @@ int nxec_scatter_chunks(nxec_ctx_t *ctx, const unsigned char *d_src, int64_t src
     if ((rc = hip_check(hipEventSynchronize(done[s]), "scatter piece sync"))) break;
     const int64_t first = p * fp.per, count = std::min(fp.per, fp.items - first);
     frame_copies(fp, first, count, slots[s]->h, HostLane::kOut, ctx->numa_node, [&](int64_t item, int64_t o, int64_t nb, uint8_t *stage) {
-      std::memcpy(h_chunks[fp.chunk(item)] + fp.off(item) + o, stage, size_t(nb));
+      unstage_copy(h_chunks[fp.chunk(item)] + fp.off(item) + o, stage, size_t(nb));
     });
   }
   hipError_t e = hipStreamSynchronize(st);

@@ -54,6 +54,8 @@ bool test_fault(const char *name);
 // ---- host memory ----
 // Copy into pinned staging (streaming stores with the NT-staging probe).
 void stage_copy(void *dst, const void *src, size_t n);
+// Copy out of pinned staging into a caller's buffer (streaming stores with the NT-staging probe).
+void unstage_copy(void *dst, const void *src, size_t n);
 // Device address of pinned / registered host memory (kernels read and write
 // it over PCIe: zero copy), or nullptr for pageable memory or when the
 // deployment turned zero copy off.

@@ -32,7 +32,7 @@ struct Tuning {
   int md5_depth = 2, md5_group = 8;  // NXEC_MD5_CFG=D,G[,NT]: k_md5 ring depth / blocks per group
   bool md5_nt = false;
   // host paths (nxec_agent.cpp, nxec_host_encode.cpp)
-  bool nt_staging = false;    // NXEC_NT_STAGING=1: streaming stores into pinned staging
+  bool nt_staging = false;    // NXEC_NT_STAGING=1: streaming stores into pinned staging and out of it
   bool host_lanes = false;    // NXEC_HOST_LANES=1: a host-pool worker set per copy direction
   bool agent_fused = true;    // NXEC_AGENT_FUSED=0: H2D -> multiply -> MD5 -> D2H batches
   bool agent_aggregate = true;  // NXEC_AGENT_AGGREGATE=0: every agent call its own round

@@ -42,11 +42,14 @@ if has frames; then
     for v in ${FRAMES_VARIANTS:-product bound lanes_bound}; do
       case $v in
         product) env="";;
+        dma) env="FRAMES_DMA=1";;
         bound) env="FRAMES_BIND=1";;
         lanes) env="NXEC_LIB=build/ab/lanes/libnxec.so NXEC_HOST_LANES=1";;
         lanes_bound) env="NXEC_LIB=build/ab/lanes/libnxec.so NXEC_HOST_LANES=1 FRAMES_BIND=1";;
         lanes7) env="NXEC_LIB=build/ab/lanes/libnxec.so NXEC_HOST_LANES=1 NXEC_HOST_THREADS=7";;
         threads12) env="NXEC_HOST_THREADS=12";;
+        nt) env="NXEC_LIB=build/ab/lanes/libnxec.so NXEC_NT_STAGING=1";;
+        probe) env="NXEC_LIB=build/ab/lanes/libnxec.so";;
       esac
       env $env timeout -k 10 200 python tools/read_frames_ab.py $v >> $OUT/frames_ab.jsonl 2>> $OUT/frames_ab.err \
         || { tail -20 $OUT/frames_ab.err; stop "frames $v" $?; }
