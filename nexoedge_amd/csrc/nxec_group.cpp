@@ -33,11 +33,6 @@ bool bind_thread_cpus(const std::vector<int> &cpus);
 
 namespace {
 
-// streams per device when a device is listed more than once: two kernels in
-// flight hide each other's ramp-up and drain, more interleave their
-// workgroups (r06 on one MI355X, 8 members: one stream each 28-72 ms per
-// step, one shared stream 20.75, against 19.3 for 8 processes)
-constexpr int kGroupStreams = 2;
 
 struct MemberThread {
   int device = 0;
@@ -173,6 +168,11 @@ int nxec_group_create(const int *devices, int ndevices, nxec_group_t **out) {
     // the device's first kGroupStreams members keep their own streams, later
     // ones take them in turn
     m->stream = nxec_ctx_stream(c);
+    // (streams per device: two kernels in flight hide each other's ramp-up
+    // and drain, many interleave their workgroups -- 8 members on one MI355X:
+    // a stream each 28-72 ms per step, one shared 20.75, two 20.1-20.6,
+    // against 19.3 for 8 processes; profiles/r06_group_hwq.log)
+    const int kGroupStreams = nxec::tuning().group_streams;
     int same = 0;
     for (MemberThread *o : g->members) same += o->device == m->device;
     if (same >= kGroupStreams) {

@@ -91,6 +91,17 @@ if has group; then
     python3 -c "import json; d=json.load(open('$OUT/group_q$q.json')); print('hwq $q ranks', d['value'], d['ms_per_step'], 'group', d['group']['value'], d['group']['ms_per_step'])"
   done
 fi
+if has gstreams; then
+  # streams per device of the 8-member one-GPU group (probe build, NXEC_GROUP_STREAMS)
+  for r in 1 2; do
+    for gs in ${GSTREAMS:-1 2 4}; do
+      NXEC_LIB=build/ab/lanes/libnxec.so NXEC_GROUP_STREAMS=$gs timeout -k 10 400 python bench.py --gpus 8 --group \
+        --stripes 512 --steps 10 --warmup 2 --no-cpu-baseline --no-host-inclusive > $OUT/gs_$gs.json 2> $OUT/gs_$gs.err \
+        || { tail -20 $OUT/gs_$gs.err; stop "gstreams $gs" $?; }
+      python3 -c "import json; d=json.load(open('$OUT/gs_$gs.json')); print('group_streams $gs ranks', d['value'], d['ms_per_step'], 'group', d['group']['value'], d['group']['ms_per_step'])" | tee -a $OUT/gstreams.log
+    done
+  done
+fi
 if has dropin; then
   for r in 1 2; do
     for v in all current; do
