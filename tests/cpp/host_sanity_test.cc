@@ -350,6 +350,30 @@ static void files_slot_plan() {
   std::printf("files slot plans: 300 checked, %d against the list-scheduling bound\n", bound_checked);
 }
 
+// The default pool of the drop-in (nxec_context.cpp): reconfigured, queried
+// and leased from many threads at once.  Without a device every lease fails
+// with NXEC_ERR_NODEV (in list mode after picking a member); the sanitizers
+// check the pool's locks, counters and the lease's release on that path.
+static void default_pool(int t) {
+  const unsigned char coef[2] = {1, 1};
+  unsigned char a[64] = {0}, b[64] = {0}, out[64];
+  const unsigned char *src[2] = {a, b};
+  unsigned char *dst[1] = {out};
+  const int lists[3][3] = {{0, 0, 0}, {0, 1, 0}, {2, 2, 2}};
+  for (int it = 0; it < 200; it++) {
+    if ((it + t) % 50 == 0) CHECK(nxec_default_devices(lists[(it + t) % 3], 1 + (it + t) % 3) == NXEC_OK, "configure");
+    if ((it + t) % 97 == 0) CHECK(nxec_default_devices(nullptr, (it % 2) ? -1 : 0) == NXEC_OK, "configure all/current");
+    const int rc = nxec_encode_host(64, 2, 1, coef, src, dst);
+    CHECK(rc == NXEC_ERR_NODEV || rc == NXEC_ERR_HIP, "no device: the lease fails cleanly (%d)", rc);
+    int dv[8], nd[8], inf[8], cnt = 0;
+    unsigned long long calls[8];
+    CHECK(nxec_default_pool_stats(dv, nd, calls, inf, 8, &cnt) == NXEC_OK, "stats");
+    const int in[4] = {it % 3, 1, 0, 2}, nodes[4] = {0, 0, 1, 1};
+    const int pick = nxec_default_pick(4, in, nodes, t % 2, it % 4);
+    CHECK(pick >= 0 && pick < 4, "pick in range");
+  }
+}
+
 int main() {
   gf_and_planning();
   files_slot_plan();
@@ -363,6 +387,16 @@ int main() {
   for (int t = 0; t < 12; t++) dt.emplace_back(digest_pool, t);
   for (auto &t : dt) t.join();
   nxec_set_digest_placement(prev);
+  std::vector<std::thread> pt;
+  for (int t = 0; t < 8; t++) pt.emplace_back(default_pool, t);
+  for (auto &t : pt) t.join();
+  // every lease released: nothing left in flight
+  {
+    int dv[16], nd[16], inf[16], cnt = 0;
+    unsigned long long calls[16];
+    CHECK(nxec_default_pool_stats(dv, nd, calls, inf, 16, &cnt) == NXEC_OK, "final stats");
+    for (int i = 0; i < cnt && i < 16; i++) CHECK(inf[i] == 0, "member %d still has %d calls in flight", i, inf[i]);
+  }
   std::printf("%s %d failures\n", g_fail ? "FAILED" : "PASSED", g_fail.load());
   return g_fail ? 1 : 0;
 }
