@@ -150,3 +150,35 @@ def test_pool_reconfiguration_and_python_callers():
     assert pool[1:] == ["3", "120", "0", "0"], pool
     cur = [l for l in r.stdout.splitlines() if l.startswith("CURRENT")][0].split()
     assert int(cur[1]) >= 1, cur
+
+
+_ENV_POOL = r"""
+import sys
+sys.path.insert(0, {root!r})
+import numpy as np
+from nexoedge_amd import nxec
+n, k = 14, 10
+enc = nxec.gen_rs_matrix(n, k)[k:]
+try:
+    nxec.encode_host(enc, [np.zeros(4096, np.uint8)] * k)
+    st = nxec.default_pool_stats()
+    print("POOL", len(st), [s["device"] for s in st], sum(s["calls"] for s in st))
+except nxec.NxecError as e:
+    print("ERROR", e.code)
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("value,want", [("0,0", "POOL 2 [0, 0] 1"), ("current", "POOL 1 [0] 1"),
+                                        ("all", "POOL 1 [0] 1"), ("0,x", "ERROR -2")])
+def test_default_devices_setting(value, want):
+    """NXEC_DEFAULT_DEVICES (INTEGRATION.md deployment settings): a device
+    list makes one member per entry, `current` and `all` one member on the
+    one-GPU box, a malformed value fails the call with NXEC_ERR_INVALID
+    instead of guessing."""
+    env = dict(os.environ, NXEC_DEFAULT_DEVICES=value)
+    r = subprocess.run(["python", "-c", _ENV_POOL.format(root=ROOT)], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith(("POOL", "ERROR"))][0]
+    assert line == want, line
