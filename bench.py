@@ -220,17 +220,17 @@ def cpu_baseline(args, n, k, cs):
 
 
 PMC_SUMMARIES = {  # (workload, chunk, layout) -> labelled per-dispatch PMC file (tools/pmc_label.py) and its op
-    # round-5 passes on the shipped library (tools/archive/gpu_r05_final.sh; every dispatch
+    # round-6 passes on the shipped library (tools/gpu_r06_final.sh; every dispatch
     # of the roofline kernel labelled with the bench line's bytes per launch);
     # tests/test_bench_line.py checks each file's labels and reports its lib_sha16
     # against libnxec.so; only the default layout the passes ran with (other
     # layouts report traffic null)
-    ("rs10_4", 1 << 20, "auto"): ("r05_pmc_rs10_4.json", "encode_recover"),
-    ("decode_full", 1 << 20, "auto"): ("r05_pmc_decode_full.json", "decode_full"),
-    ("mixed16", 4 << 20, "auto"): ("r05_pmc_mixed16.json", "encode_recover"),
-    ("write14", 1 << 20, "auto"): ("r05_pmc_write14.json", "encode_md5_fused"),
-    ("repair12", 1 << 20, "auto"): ("r05_pmc_repair12.json", "repair_fused_perm12"),
-    ("files", 1 << 20, "auto"): ("r05_pmc_files.json", "encode_objects_md5"),
+    ("rs10_4", 1 << 20, "auto"): ("r06_pmc_rs10_4.json", "encode_recover"),
+    ("decode_full", 1 << 20, "auto"): ("r06_pmc_decode_full.json", "decode_full"),
+    ("mixed16", 4 << 20, "auto"): ("r06_pmc_mixed16.json", "encode_recover"),
+    ("write14", 1 << 20, "auto"): ("r06_pmc_write14.json", "encode_md5_fused"),
+    ("repair12", 1 << 20, "auto"): ("r06_pmc_repair12.json", "repair_fused_perm12"),
+    ("files", 1 << 20, "auto"): ("r06_pmc_files.json", "encode_objects_md5"),
 }
 
 
