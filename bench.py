@@ -19,6 +19,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -1004,6 +1005,13 @@ def main():
             result["host_inclusive"] = hi
     if args.host_inclusive and headline_n1:
         result["host_inclusive"] = host_inclusive(ctx, args.n, args.k, args.chunk)
+    if args.host_inclusive and wl.name == "rs10_4":
+        # the unmodified drop-in over every visible GPU (one process, the
+        # default pool), rank 0 only while the other ranks wait
+        grp.barrier()
+        if rank == 0:
+            result.setdefault("host_inclusive", {})["dropin_pool"] = dropin_pool_rate(orig_affinity)
+        grp.barrier()
     if (headline_n1 or (rank == 0 and world == 1 and wl.name == "config1")) and not args.no_cpu_baseline:
         os.sched_setaffinity(0, orig_affinity)  # the host's CPUs, not only the GPU's node
     if headline_n1 and not args.no_cpu_baseline:
@@ -1079,6 +1087,42 @@ def host_inclusive(ctx, n, k, cs, ns=512):
     out["read_frames_decode_GiB_s_user_data"] = rf["pipelined"]
     out["read_frames_decode_legs"] = rf
     out["recover_frames_zero_copy"] = recover_frames_rate(ctx, n, k, cs, min(ns, 128))
+    return out
+
+
+def dropin_pool_rate(affinity, threads="16,64", secs="1.5"):
+    """The per-stripe drop-in as an unmodified proxy runs it -- RSCode::decode
+    (4 erasures) and CodingUtils::encode per stripe with pageable buffers from
+    16 and 64 caller threads sharing one RSCode -- in a child process
+    (build/dropin_rate pool, tools/dropin_rate.cc) whose default pool holds a
+    context per visible GPU: on an N-GPU node the calls spread
+    over N PCIe links.  GiB/s of (k+p)*cs resp. (k+e)*cs per stripe, and the
+    calls each pool member served.  Host CPUs: the process's original
+    affinity (not only GPU 0's node)."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "dropin_rate")
+    if not os.path.exists(exe):
+        return {"skipped": "build/dropin_rate not built"}
+    mine = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, affinity)  # the child inherits it
+    try:
+        r = subprocess.run([exe, str(1 << 20), secs, "pool", threads], capture_output=True, text=True, timeout=180)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    finally:
+        os.sched_setaffinity(0, mine)
+    out = {"legs": [], "note": "per-stripe RSCode::decode / CodingUtils::encode, pageable buffers, one process, "
+                               "default pool over every visible GPU (NXEC_DEFAULT_DEVICES=all)"}
+    for line in r.stdout.splitlines():
+        try:
+            d = json.loads(line)
+        except ValueError:
+            continue
+        if "pool_members" in d:
+            out["pool_members"] = d["pool_members"]
+        elif "path" in d:
+            out["legs"].append({"path": d["path"], "threads": d["threads"], "GiB_s": d["GiB_s"], "ok": d["ok"]})
+    if r.returncode != 0:
+        out["error"] = f"rc {r.returncode}: {r.stderr[-300:]}"
     return out
 
 

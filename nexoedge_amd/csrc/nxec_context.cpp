@@ -568,7 +568,33 @@ int member_ctx(Member *m, nxec_ctx_t **out) {
 
 }  // namespace
 
+namespace {
+// Per-device admission (the pool_admit probe): at most that many drop-in calls
+// run on a device at once; the rest wait here instead of piling staging slots
+// and streams onto the device's hardware queues.
+struct DeviceGate {
+  std::mutex mu;
+  std::condition_variable cv;
+  int running = 0;
+};
+DeviceGate &device_gate(int device) {
+  static std::mutex mu;
+  static std::deque<DeviceGate> gates;  // stable addresses
+  std::lock_guard<std::mutex> lk(mu);
+  while (static_cast<int>(gates.size()) <= device) gates.emplace_back();
+  return gates[device];
+}
+}  // namespace
+
 DefaultLease::~DefaultLease() {
+  if (gate_) {
+    DeviceGate *g = static_cast<DeviceGate *>(gate_);
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      g->running--;
+    }
+    g->cv.notify_one();
+  }
   if (member_) static_cast<Member *>(member_)->inflight.fetch_sub(1, std::memory_order_relaxed);
   int cur = -1;
   if (saved_device_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != saved_device_) (void)hipSetDevice(saved_device_);
@@ -604,6 +630,14 @@ int default_ctx(DefaultLease &lease) {
   m->calls.fetch_add(1, std::memory_order_relaxed);
   lease.member_ = m;
   lease.saved_device_ = saved;
+  int admitted = 0;
+  if (const int cap = tuning().pool_admit; cap > 0) {
+    DeviceGate &g = device_gate(m->device);
+    std::unique_lock<std::mutex> lk(g.mu);
+    g.cv.wait(lk, [&] { return g.running < cap; });
+    admitted = ++g.running;
+    lease.gate_ = &g;
+  }
   nxec_ctx_t *c = nullptr;
   if (int rc = member_ctx(m, &c)) return rc;
   lease.ctx = c;
@@ -617,7 +651,7 @@ int default_ctx(DefaultLease &lease) {
     for (Member *o : cfg->members)
       if (o->device == m->device) dev_inflight += o->inflight.load(std::memory_order_relaxed);
   }
-  lease.device_inflight = std::max(1, dev_inflight);
+  lease.device_inflight = std::max(1, admitted ? admitted : dev_inflight);
   return NXEC_OK;
 }
 

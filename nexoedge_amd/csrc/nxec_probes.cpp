@@ -37,6 +37,7 @@ Tuning read_tuning() {
   if ((e = knob("NXEC_NT_STAGING"))) t.nt_staging = e[0] == '1';
   if ((e = knob("NXEC_HOST_LANES"))) t.host_lanes = e[0] == '1';
   if ((e = knob("NXEC_GROUP_STREAMS"))) t.group_streams = std::max(1, std::atoi(e));
+  if ((e = knob("NXEC_POOL_ADMIT"))) t.pool_admit = std::max(0, std::atoi(e));
   if ((e = knob("NXEC_AGENT_FUSED"))) t.agent_fused = e[0] != '0';
   if ((e = knob("NXEC_AGENT_AGGREGATE"))) t.agent_aggregate = e[0] != '0';
   if ((e = knob("NXEC_AGENT_BATCH_MB"))) t.agent_batch_mb = std::atoi(e);

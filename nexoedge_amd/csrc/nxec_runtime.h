@@ -184,6 +184,7 @@ class DefaultLease {
  private:
   friend int default_ctx(DefaultLease &lease);
   void *member_ = nullptr;
+  void *gate_ = nullptr;  // the device's admission gate this call holds (pool_admit)
   int saved_device_ = -1;
 };
 int default_ctx(DefaultLease &lease);

@@ -16,7 +16,7 @@
 // stripe), the unit of bench.py cpu_baseline.write_path_with_md5.  Run it with
 // NXEC_CHUNK_MD5=0 for the host-hashed (OpenSSL) form.
 //
-// usage: dropin_rate [cs] [seconds] [all|agent|write] [threads,...]
+// usage: dropin_rate [cs] [seconds] [all|agent|write|pool] [threads,...]
 // Build: make tools   (build/dropin_rate)
 #include <algorithm>
 #include <atomic>
@@ -48,6 +48,10 @@ int main(int argc, char **argv) {
   // argv[3] = "agent": only the agent-service leg; "write": only the writeFileStripe leg
   const bool agent_only = argc > 3 && std::strcmp(argv[3], "agent") == 0;
   const bool write_only = argc > 3 && std::strcmp(argv[3], "write") == 0;
+  // "pool": only RSCode::decode and CodingUtils::encode, then the default
+  // pool's members (device, NUMA node, calls served) -- the drop-in spread
+  // over every visible GPU (bench.py host_inclusive.dropin_pool)
+  const bool pool_only = argc > 3 && std::strcmp(argv[3], "pool") == 0;
   std::vector<int> tlist0{1, 4, 16};
   if (argc > 4) {
     tlist0.clear();
@@ -58,7 +62,7 @@ int main(int argc, char **argv) {
     }
   }
   // one timed leg of path `op` with `threads` callers; prints its line, returns GiB/s
-  auto leg = [&](int threads, int op, double secs) -> double {
+  auto leg = [&](int threads, int op, double secs, bool quiet = false) -> double {
       std::atomic<long> stripes{0};
       std::atomic<bool> ok{true};
       unsigned long long h0 = 0, g0 = 0, h1 = 0, g1 = 0;
@@ -129,12 +133,13 @@ int main(int argc, char **argv) {
       const double bytes = static_cast<double>(stripes) * (op == 3 ? k : k + (op != 1 ? n - k : e)) * cs;
       static const char *names[4] = {"RSCode::encode", "RSCode::decode", "CodingUtils::encode", "writeFileStripe"};
       static const char *place_names[4] = {"auto", "gpu", "host", "?"};
-      std::printf("{\"path\": \"%s per stripe\", \"threads\": %d, \"chunk\": %d, \"stripes\": %ld, "
-                  "\"GiB_s%s\": %.2f, \"ms_per_call\": %.3f, \"chunk_md5\": %d, \"digest_place\": \"%s\", "
-                  "\"digest_calls_host\": %llu, \"digest_calls_gpu\": %llu, \"digest_threads\": %d, \"ok\": %s}\n",
-                  names[op], threads, cs, static_cast<long>(stripes), op == 3 ? "_user_data" : "",
-                  bytes / dt / (1 << 30), 1e3 * dt * threads / static_cast<double>(stripes), nxec_chunk_md5_mode(),
-                  place_names[nxec_digest_placement() & 3], h1 - h0, g1 - g0, dthreads, ok ? "true" : "false");
+      if (!quiet)
+        std::printf("{\"path\": \"%s per stripe\", \"threads\": %d, \"chunk\": %d, \"stripes\": %ld, "
+                    "\"GiB_s%s\": %.2f, \"ms_per_call\": %.3f, \"chunk_md5\": %d, \"digest_place\": \"%s\", "
+                    "\"digest_calls_host\": %llu, \"digest_calls_gpu\": %llu, \"digest_threads\": %d, \"ok\": %s}\n",
+                    names[op], threads, cs, static_cast<long>(stripes), op == 3 ? "_user_data" : "",
+                    bytes / dt / (1 << 30), 1e3 * dt * threads / static_cast<double>(stripes), nxec_chunk_md5_mode(),
+                    place_names[nxec_digest_placement() & 3], h1 - h0, g1 - g0, dthreads, ok ? "true" : "false");
       std::fflush(stdout);
       return bytes / dt / (1 << 30);
   };
@@ -184,10 +189,32 @@ int main(int argc, char **argv) {
     delete code;
     return 0;
   }
+  if (pool_only) {  // warm-up: every member's staging slots and the arena pinned before timing
+    int tmax = 1;
+    for (int t : tlist0) tmax = std::max(tmax, t);
+    leg(tmax, 2, 0.5, true);
+    leg(tmax, 1, 0.5, true);
+  }
   for (int threads : tlist0) {
     if (agent_only) break;
+    if (pool_only) {
+      leg(threads, 2, secs);
+      leg(threads, 1, secs);
+      continue;
+    }
     for (int op = write_only ? 3 : 0; op < 4; op++)  // 0 RSCode::encode, 1 RSCode::decode, 2 CodingUtils::encode,
       leg(threads, op, secs);                        // 3 writeFileStripe (encode + MD5 of every chunk + events)
+  }
+  if (pool_only) {
+    int dv[64], nd[64], inf[64], cnt = 0;
+    unsigned long long served[64];
+    nxec_default_pool_stats(dv, nd, served, inf, 64, &cnt);
+    std::printf("{\"pool_members\": [");
+    for (int i = 0; i < cnt && i < 64; i++)
+      std::printf("%s{\"device\": %d, \"node\": %d, \"calls\": %llu}", i ? ", " : "", dv[i], nd[i], served[i]);
+    std::printf("]}\n");
+    delete code;
+    return 0;
   }
   if (write_only) {
     delete code;

@@ -102,6 +102,19 @@ if has gstreams; then
     done
   done
 fi
+if has admit; then
+  # per-device admission of drop-in calls (probe build, NXEC_POOL_ADMIT; 0 = none), 16 / 64 callers
+  for r in 1 2; do
+    for a in ${ADMIT:-0 8 16}; do
+      LD_LIBRARY_PATH=$(pwd)/build/ab/lanes NXEC_POOL_ADMIT=$a timeout -k 10 200 build/dropin_rate 1048576 1.5 pool 16,64 \
+        | sed "s/^{/{\"admit\": $a, /" >> $OUT/admit_ab.jsonl 2>> $OUT/admit_ab.err || { tail -20 $OUT/admit_ab.err; stop "admit $a" $?; }
+    done
+  done
+  grep GiB_s $OUT/admit_ab.jsonl | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('admit', d['admit'], d['path'][:22], d['threads'], d['GiB_s'])"
+fi
 if has dropin; then
   for r in 1 2; do
     for v in all current; do
