@@ -569,9 +569,12 @@ int member_ctx(Member *m, nxec_ctx_t **out) {
 }  // namespace
 
 namespace {
-// Per-device admission (the pool_admit probe): at most that many drop-in calls
-// run on a device at once; the rest wait here instead of piling staging slots
-// and streams onto the device's hardware queues.
+// Per-device admission (tuning().pool_admit, 8): at most that many drop-in
+// calls run on a device at once; the rest wait here instead of piling staging
+// slots, streams and host-pool copies onto one device (64 callers on one GPU:
+// CodingUtils::encode 21 -> 64 GiB/s, RSCode::decode 14 -> 62; 16 callers
+// 56 -> 67; profiles/r06_admit_ab.jsonl).  The pick above already counted
+// this call, so later callers go to a less busy member while this one waits.
 struct DeviceGate {
   std::mutex mu;
   std::condition_variable cv;

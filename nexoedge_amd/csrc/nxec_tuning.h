@@ -35,7 +35,7 @@ struct Tuning {
   bool nt_staging = false;    // NXEC_NT_STAGING=1: streaming stores into pinned staging and out of it
   bool host_lanes = false;    // NXEC_HOST_LANES=1: a host-pool worker set per copy direction
   int group_streams = 2;      // NXEC_GROUP_STREAMS: streams per device of an nxec_group listing it repeatedly
-  int pool_admit = 0;         // NXEC_POOL_ADMIT: drop-in calls running per device at most (0 = no gate)
+  int pool_admit = 8;         // NXEC_POOL_ADMIT: drop-in calls running per device at most (0 = no gate)
   bool agent_fused = true;    // NXEC_AGENT_FUSED=0: H2D -> multiply -> MD5 -> D2H batches
   bool agent_aggregate = true;  // NXEC_AGENT_AGGREGATE=0: every agent call its own round
   int agent_batch_mb = 0;     // NXEC_AGENT_BATCH_MB: staging per agent batch (0 = the caller's)

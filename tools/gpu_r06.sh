@@ -106,7 +106,7 @@ if has admit; then
   # per-device admission of drop-in calls (probe build, NXEC_POOL_ADMIT; 0 = none), 16 / 64 callers
   for r in 1 2; do
     for a in ${ADMIT:-0 8 16}; do
-      LD_LIBRARY_PATH=$(pwd)/build/ab/lanes NXEC_POOL_ADMIT=$a timeout -k 10 200 build/dropin_rate 1048576 1.5 pool 16,64 \
+      LD_LIBRARY_PATH=$(pwd)/build/ab/lanes NXEC_POOL_ADMIT=$a timeout -k 10 200 build/dropin_rate 1048576 1.5 pool ${ADMIT_THREADS:-16,64} \
         | sed "s/^{/{\"admit\": $a, /" >> $OUT/admit_ab.jsonl 2>> $OUT/admit_ab.err || { tail -20 $OUT/admit_ab.err; stop "admit $a" $?; }
     done
   done
