@@ -111,6 +111,13 @@ int nxec_default_pool_stats(int *devices, int *nodes, unsigned long long *calls,
  * flight; on an exact tie `prev` (the member this thread used last; -1
  * none), else the lowest index.  Pure (no device); returns the index. */
 int nxec_default_pick(int n, const int *inflight, const int *nodes, int caller_node, int prev);
+/* Per-device admission of the calls above: at most *limit (8) run on one
+ * device at once, later callers wait for a place (they were already counted
+ * by the pick, so the next caller goes to a less busy member).  Reads the
+ * device's gate: calls running now, the most that ran at once, calls that
+ * found it full; reset != 0 restarts peak and waited.  (64 callers on one
+ * GPU: 14-22 GiB/s unbounded, 62-66 with 8) */
+int nxec_default_admission(int device, int *limit, int *running, int *peak, unsigned long long *waited, int reset);
 
 /* nxec_encode_host plus fused pass-through: for j < k with copy_idx[j] >= 0,
  * data[j] is also delivered to copy_out[copy_idx[j]] by the same GPU pass

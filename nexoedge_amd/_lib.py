@@ -49,6 +49,7 @@ _PROTOS = {
     "nxec_default_devices": (C.c_int, [vp, C.c_int]),
     "nxec_default_pool_stats": (C.c_int, [vp, vp, vp, vp, C.c_int, vp]),
     "nxec_default_pick": (C.c_int, [C.c_int, vp, vp, C.c_int, C.c_int]),
+    "nxec_default_admission": (C.c_int, [C.c_int, vp, vp, vp, vp, C.c_int]),
     "nxec_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
     "nxec_ctx_destroy": (None, [vp]),
     "nxec_ctx_stream": (vp, [vp]),

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -579,6 +580,8 @@ struct DeviceGate {
   std::mutex mu;
   std::condition_variable cv;
   int running = 0;
+  int peak = 0;                 // most calls running at once (nxec_default_admission)
+  unsigned long long waited = 0;  // calls that found the gate full
 };
 DeviceGate &device_gate(int device) {
   static std::mutex mu;
@@ -637,10 +640,14 @@ int default_ctx(DefaultLease &lease) {
   if (const int cap = tuning().pool_admit; cap > 0) {
     DeviceGate &g = device_gate(m->device);
     std::unique_lock<std::mutex> lk(g.mu);
+    if (g.running >= cap) g.waited++;
     g.cv.wait(lk, [&] { return g.running < cap; });
     admitted = ++g.running;
+    g.peak = std::max(g.peak, admitted);
     lease.gate_ = &g;
   }
+  // testing (NXEC_TEST_FAULT=admit_stall): hold the place 30 ms so callers queue
+  if (admitted && test_fault("admit_stall")) std::this_thread::sleep_for(std::chrono::milliseconds(30));
   nxec_ctx_t *c = nullptr;
   if (int rc = member_ctx(m, &c)) return rc;
   lease.ctx = c;
@@ -790,6 +797,23 @@ int nxec_default_pool_stats(int *devices, int *nodes, unsigned long long *calls,
     nodes[i] = ms[i]->node;
     calls[i] = ms[i]->calls.load(std::memory_order_relaxed);
     inflight[i] = ms[i]->inflight.load(std::memory_order_relaxed);
+  }
+  return NXEC_OK;
+}
+
+int nxec_default_admission(int device, int *limit, int *running, int *peak, unsigned long long *waited, int reset) {
+  int count = 0;
+  if (device < 0 || hipGetDeviceCount(&count) != hipSuccess || device >= count)
+    return set_error(NXEC_ERR_INVALID, "nxec_default_admission: no device %d", device);
+  DeviceGate &g = device_gate(device);
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (limit) *limit = tuning().pool_admit;
+  if (running) *running = g.running;
+  if (peak) *peak = g.peak;
+  if (waited) *waited = g.waited;
+  if (reset) {
+    g.peak = g.running;
+    g.waited = 0;
   }
   return NXEC_OK;
 }

@@ -246,6 +246,16 @@ def default_pool_stats() -> list:
     return [{"device": dv[i], "node": nd[i], "calls": calls[i], "inflight": inf[i]} for i in range(min(n, cnt.value))]
 
 
+def default_admission(device: int = 0, reset: bool = False) -> dict:
+    """nxec_default_admission: the device's admission gate of the default
+    pool -- {limit, running, peak, waited}; reset restarts peak and waited."""
+    lim, run, peak = C.c_int(), C.c_int(), C.c_int()
+    waited = C.c_ulonglong()
+    check(lib.nxec_default_admission(int(device), C.byref(lim), C.byref(run), C.byref(peak), C.byref(waited),
+                                     int(bool(reset))), "nxec_default_admission")
+    return {"limit": lim.value, "running": run.value, "peak": peak.value, "waited": waited.value}
+
+
 def default_pick(inflight: Sequence[int], nodes: Optional[Sequence[int]] = None, caller_node: int = -1,
                  prev: int = -1) -> int:
     """nxec_default_pick: the member the default pool leases for one call."""

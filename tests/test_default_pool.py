@@ -182,3 +182,49 @@ def test_default_devices_setting(value, want):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith(("POOL", "ERROR"))][0]
     assert line == want, line
+
+
+_ADMIT = r"""
+import sys, threading
+sys.path.insert(0, {root!r})
+import numpy as np
+import oracle
+from nexoedge_amd import nxec
+nxec.default_devices([0, 0, 0, 0])
+n, k, cs = 14, 10, (256 << 10) + 16
+enc = nxec.gen_rs_matrix(n, k)[k:]
+nxec.default_admission(0, reset=True)
+inputs = [[np.random.default_rng(100 * t + i).integers(0, 256, cs, dtype=np.uint8) for i in range(k)]
+          for t in range(24)]
+errs, go = [], threading.Barrier(24)
+def worker(t):
+    go.wait()
+    for it in range(3):
+        got = nxec.encode_host(enc, inputs[t])
+        if not all(np.array_equal(g, w) for g, w in zip(got, oracle.matmul(enc, inputs[t]))):
+            errs.append((t, it))
+th = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+[x.start() for x in th]
+[x.join() for x in th]
+a = nxec.default_admission(0)
+print("ADMIT", a["limit"], a["running"], a["peak"], int(a["waited"] > 0), len(errs))
+"""
+
+
+@pytest.mark.gpu
+def test_admission_bounds_calls_per_device():
+    """Per-device admission: 24 threads through a 4-member pool
+    on the one device, each admitted call held 30 ms (NXEC_TEST_FAULT=
+    admit_stall) -- never more than 8 run at once, the gate fills (callers
+    waited) and drains (none running after), every encode bit-exact."""
+    env = dict(os.environ, NXEC_TEST_FAULT="admit_stall")
+    r = subprocess.run(["python", "-c", _ADMIT.format(root=ROOT)], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("ADMIT")][0].split()
+    assert line[1:] == ["8", "0", "8", "1", "0"], line
+
+
+def test_admission_rejects_bad_device():
+    with pytest.raises(nxec.NxecError):
+        nxec.default_admission(-1)
