@@ -115,6 +115,19 @@ import json,sys
 for l in sys.stdin:
     d=json.loads(l); print('admit', d['admit'], d['path'][:22], d['threads'], d['GiB_s'])"
 fi
+if has tunedab; then
+  # config 5: --layout auto and --layout tuned interleaved (same strides chosen; does the calibration's
+  # 24 GiB scratch, freed before the batch is allocated, change the batch's speed?)
+  for r in 1 2; do
+    for c in 262144 4194304; do
+      for lay in auto tuned; do
+        timeout -k 10 300 python bench.py --workload mixed16 --chunk $c --layout $lay --steps 10 --warmup 2 --no-cpu-baseline \
+          --no-host-inclusive > $OUT/tab.json 2> $OUT/tab.err || stop tunedab $?
+        python3 -c "import json; d=json.load(open('$OUT/tab.json')); print('tunedab', $r, $c, '$lay', d['roofline']['avg_launch_ms'], d['roofline']['frac'], d['config']['layout'][:60])" | tee -a $OUT/tunedab.log
+      done
+    done
+  done
+fi
 if has dropin; then
   for r in 1 2; do
     for v in all current; do
