@@ -606,7 +606,27 @@ DefaultLease::~DefaultLease() {
   if (saved_device_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != saved_device_) (void)hipSetDevice(saved_device_);
 }
 
-int default_ctx(DefaultLease &lease) {
+int lease_admit(DefaultLease &lease) {
+  const int cap = tuning().pool_admit;
+  Member *m = static_cast<Member *>(lease.member_);
+  if (cap <= 0 || !m || lease.gate_) return 0;
+  DeviceGate &g = device_gate(m->device);
+  int admitted = 0;
+  {
+    std::unique_lock<std::mutex> lk(g.mu);
+    if (g.running >= cap) g.waited++;
+    g.cv.wait(lk, [&] { return g.running < cap; });
+    admitted = ++g.running;
+    g.peak = std::max(g.peak, admitted);
+    lease.gate_ = &g;
+  }
+  // testing (NXEC_TEST_FAULT=admit_stall): hold the place 30 ms so callers queue
+  if (test_fault("admit_stall")) std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  lease.device_inflight = admitted;
+  return admitted;
+}
+
+int default_ctx(DefaultLease &lease, bool admit) {
   std::shared_ptr<const PoolCfg> cfg;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -636,18 +656,7 @@ int default_ctx(DefaultLease &lease) {
   m->calls.fetch_add(1, std::memory_order_relaxed);
   lease.member_ = m;
   lease.saved_device_ = saved;
-  int admitted = 0;
-  if (const int cap = tuning().pool_admit; cap > 0) {
-    DeviceGate &g = device_gate(m->device);
-    std::unique_lock<std::mutex> lk(g.mu);
-    if (g.running >= cap) g.waited++;
-    g.cv.wait(lk, [&] { return g.running < cap; });
-    admitted = ++g.running;
-    g.peak = std::max(g.peak, admitted);
-    lease.gate_ = &g;
-  }
-  // testing (NXEC_TEST_FAULT=admit_stall): hold the place 30 ms so callers queue
-  if (admitted && test_fault("admit_stall")) std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  const int admitted = admit ? lease_admit(lease) : 0;
   nxec_ctx_t *c = nullptr;
   if (int rc = member_ctx(m, &c)) return rc;
   lease.ctx = c;

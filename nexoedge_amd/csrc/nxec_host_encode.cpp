@@ -351,8 +351,12 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
       if (rc == NXEC_OK) digest_gpu_observe(len, (digest_clock_ns() - t0) * 1e-6);
     }
   } observe{len, rc, t_call};
+  // admitted only for the staged form below: a zero-copy call waits for a
+  // shared digest round (one launch for every pending call, ~10 ms per MiB of
+  // chain) and holds no staging of its own, so gating it would only shrink
+  // the rounds
   DefaultLease lease;
-  if ((rc = default_ctx(lease))) return rc;
+  if ((rc = default_ctx(lease, false))) return rc;
   nxec_ctx_t *ctx = lease.ctx;
   DigestJob job;
   job.len = len;
@@ -373,6 +377,7 @@ int nxec_encode_host_md5(int len, int k, int rows, const unsigned char *coeffs, 
     job.out_dv.push_back(reinterpret_cast<uintptr_t>(dv));
   }
   if (!mapped) {
+    lease_admit(lease);
     nxec_agent_req r;
     r.ninputs = k;
     r.noutputs = rows;

@@ -182,12 +182,18 @@ class DefaultLease {
   nxec_ctx_t *ctx = nullptr;
   int device_inflight = 1;  // calls in flight on ctx's device, this one included
  private:
-  friend int default_ctx(DefaultLease &lease);
+  friend int default_ctx(DefaultLease &lease, bool admit);
+  friend int lease_admit(DefaultLease &lease);
   void *member_ = nullptr;
   void *gate_ = nullptr;  // the device's admission gate this call holds (pool_admit)
   int saved_device_ = -1;
 };
-int default_ctx(DefaultLease &lease);
+// admit = false: skip the device's admission gate (a call that mostly waits
+// for a shared digest round holds no staging of its own while it waits)
+int default_ctx(DefaultLease &lease, bool admit = true);
+// The device admission of a lease taken with admit = false (no-op when it
+// already holds a place or the gate is off); returns the calls running.
+int lease_admit(DefaultLease &lease);
 inline hipStream_t pick_stream(nxec_ctx_t *ctx, void *stream) {
   return stream ? static_cast<hipStream_t>(stream) : ctx->stream;
 }

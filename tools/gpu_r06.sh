@@ -115,6 +115,24 @@ import json,sys
 for l in sys.stdin:
     d=json.loads(l); print('admit', d['admit'], d['path'][:22], d['threads'], d['GiB_s'])"
 fi
+if has admitw; then
+  # the admission gate on the write legs (RSCode::encode with the digests, writeFileStripe), 16 / 64 callers:
+  # no gate / gate on every call (build/ab/lanes_noex) / gate except zero-copy digest calls (build/ab/lanes)
+  for r in 1 2; do
+    for v in "noex 0" "noex 8" "lanes 8"; do
+      set -- $v
+      for mode in write all; do
+        LD_LIBRARY_PATH=$(pwd)/build/ab/$1 NXEC_POOL_ADMIT=$2 timeout -k 10 200 build/dropin_rate 1048576 1.5 $mode ${ADMIT_THREADS:-16,64} \
+          | sed "s/^{/{\"variant\": \"$1\", \"admit\": $2, /" >> $OUT/admitw_ab.jsonl 2>> $OUT/admitw_ab.err || { tail -20 $OUT/admitw_ab.err; stop "admitw $v $mode" $?; }
+      done
+    done
+  done
+  grep -h GiB_s $OUT/admitw_ab.jsonl | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l)
+    if 'path' in d and 'threads' in d: print('admitw', d['variant'], d['admit'], d['path'][:26], d.get('buffers',''), d['threads'], d.get('GiB_s', d.get('GiB_s_user_data')), d.get('digest_calls_host'), d.get('digest_calls_gpu'))"
+fi
 if has tunedab; then
   # config 5: --layout auto and --layout tuned interleaved (same strides chosen; does the calibration's
   # 24 GiB scratch, freed before the batch is allocated, change the batch's speed?)
